@@ -1,0 +1,355 @@
+#!/usr/bin/env python3
+"""bench.py -- MFCC frames/s of the level-2 scorer (+ streaming level-1 gate)
+on MI355X, next to the CPU oracle on the host cores.
+
+Contract (see the task's bench section): ``python bench.py --gpus N --steps K
+--warmup W``; for N>1 it is launched under torch.distributed.run, one rank per
+GPU (RCCL).  Rank 0 prints ONE JSON line.
+
+Workload (BASELINE.json configs[1], "1024 concurrent synthetic 16 kHz streams,
+MFCC+cosine match, 1xMI355X"): per GPU, 1024 streams x 64 gated segments =
+65536 ragged segments with L ~ U{6400..33600} samples, resident
+in HBM as one fp32 buffer.  Half the segments carry the reference word (gain
+U(0.2,3), noise sigma U(1e-4,5e-3)), a quarter an 880 Hz burst, a quarter the
+time-reversed word, so both decisions occur.  A step = one scorer pass over the
+whole batch: MFCC (stft+mel+log+top_db+DCT), mean/std, cosine score, match,
+and the fp64 re-score of near-threshold segments.  For N>1 the step also
+all-gathers every rank's (score, match) to rank 0 over RCCL -- the gather of
+positive detections that feeds the optional Whisper confirm.
+Streams shard across ranks (weak scaling).
+
+Extra fields: ``roofline`` (dominant kernel k_score_f32, 640 algorithmic bytes
+per MFCC frame, HIP-event timed), ``cpu_baseline`` (oracle/mfcc_ref.py, the
+librosa-0.11 restatement, on rank 0 at N=1 only, time-bounded sample),
+``streaming`` (configs[2]: 8192 streams through the full level-1 + level-2
+engine, per-tick launches, real-time capacity).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "real-time 16 kHz streams sustained + MFCC frames/sec at 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BYTES_PER_FRAME = 640          # 160 new fp32 samples per MFCC frame
+HOP = 160
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--streams", type=int, default=1024, help="streams per GPU (config 2)")
+    ap.add_argument("--segments-per-stream", type=int, default=64)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-streaming", action="store_true")
+    ap.add_argument("--stream-count", type=int, default=8192, help="config 3 streams per GPU")
+    ap.add_argument("--stream-ticks", type=int, default=600, help="ticks after the 10 s prefill")
+    return ap.parse_args()
+
+
+def load_word() -> np.ndarray:
+    import wave
+    with wave.open(os.path.join(ROOT, "tests", "golden", "reference_word.wav"), "rb") as w:
+        raw = w.readframes(w.getnframes())
+    return np.frombuffer(raw, dtype="<i2").astype(np.float32) / np.float32(32768.0)
+
+
+def make_segments(torch, dev, n_seg, seed, word):
+    """Synthetic ragged batch on the GPU (deterministic per seed)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    lengths = rng.integers(6400, 33600 + 1, n_seg).astype(np.int32)
+    offsets = np.zeros(n_seg, np.int64)
+    offsets[1:] = np.cumsum(lengths[:-1], dtype=np.int64)
+    total = int(lengths.sum())
+    sigma = rng.uniform(1e-4, 5e-3, n_seg)
+    gain = rng.uniform(0.2, 3.0, n_seg)
+    kind = rng.integers(0, 4, n_seg)             # 0,1 word; 2 tone 880 Hz; 3 reversed word
+    start = (rng.random(n_seg) * np.maximum(1, lengths - len(word))).astype(np.int64)
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    pcm = torch.randn(total, generator=g, device=dev, dtype=torch.float32)
+    seg_id = torch.repeat_interleave(torch.arange(n_seg, device=dev), torch.from_numpy(lengths.astype(np.int64)).to(dev))
+    pcm.mul_(torch.from_numpy(sigma.astype(np.float32)).to(dev)[seg_id])
+    del seg_id
+    wl = len(word)
+    wv = torch.from_numpy(word).to(dev)
+    tone = torch.from_numpy((0.3 * np.sin(2 * np.pi * 880 * np.arange(wl) / 16000)).astype(np.float32)).to(dev)
+    ar = torch.arange(wl, device=dev)
+    for c0 in range(0, n_seg, 2048):
+        c1 = min(n_seg, c0 + 2048)
+        L = torch.from_numpy(lengths[c0:c1].astype(np.int64)).to(dev)
+        base = torch.from_numpy(offsets[c0:c1] + start[c0:c1]).to(dev)
+        room = L - torch.from_numpy(start[c0:c1]).to(dev)
+        k = torch.from_numpy(kind[c0:c1]).to(dev)
+        gn = torch.from_numpy(gain[c0:c1].astype(np.float32)).to(dev)
+        src = torch.where((k <= 1)[:, None], wv[None, :],
+                          torch.where((k == 2)[:, None], tone[None, :], wv.flip(0)[None, :]))
+        val = src * gn[:, None]
+        mask = ar[None, :] < room[:, None]
+        idx = base[:, None] + ar[None, :]
+        pcm.index_put_((idx[mask],), val[mask], accumulate=True)
+    frames = int((1 + lengths.astype(np.int64) // HOP).sum())
+    return (pcm, torch.from_numpy(offsets).to(dev), torch.from_numpy(lengths).to(dev), frames,
+            lengths, offsets)
+
+
+# --------------------------------------------------------------------------- CPU baseline
+def _cpu_worker(args):
+    seg_list, seconds = args
+    os.environ["OMP_NUM_THREADS"] = "1"
+    from oracle import mfcc_ref
+    tm, ts = mfcc_ref.extract_mfcc(load_word())
+    t0 = time.perf_counter()
+    frames = 0
+    n = 0
+    for x in seg_list:
+        cm, cs = mfcc_ref.extract_mfcc(x.astype(np.float64))   # float64 candidate path (wakeword.py:1105-1121)
+        mfcc_ref.similarity_from_stats(tm, ts, cm, cs)
+        frames += 1 + len(x) // HOP
+        n += 1
+        if time.perf_counter() - t0 > seconds:
+            break
+    return frames, n, time.perf_counter() - t0
+
+
+def cpu_baseline(host_pcm, lengths, offsets, seconds):
+    import multiprocessing as mp
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    procs = max(1, min(16, cores))
+    per = 400
+    jobs = []
+    for p in range(procs):
+        idx = range(p * per, min(len(lengths), (p + 1) * per))
+        jobs.append(([host_pcm[offsets[i] - offsets[0]: offsets[i] - offsets[0] + lengths[i]] for i in idx],
+                     seconds))
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs, initializer=_pool_init) as pool:
+        res = pool.map(_cpu_worker, jobs)
+    frames = sum(r[0] for r in res)
+    segs = sum(r[1] for r in res)
+    wall = max(r[2] for r in res)
+    return {"value": frames / wall, "unit": "frames/s", "cores": procs, "kind": "port",
+            "sample": f"{segs} segments ({frames} MFCC frames) of the same ragged batch, float64 candidate path, "
+                      f"oracle/mfcc_ref.py (numpy/scipy restatement of librosa 0.11.0 mfcc + scipy cosine), "
+                      f"{procs} processes x ~{seconds:.0f} s, OMP_NUM_THREADS=1"}
+
+
+def _pool_init():
+    os.environ["OMP_NUM_THREADS"] = "1"
+    sys.path.insert(0, ROOT)
+
+
+# --------------------------------------------------------------------------- streaming (config 3)
+def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word):
+    """Full level-1 + level-2 engine on `n_streams` synthetic streams: 10 s
+    prefill, then `n_ticks` ticks launched one at a time (the real-time cadence)."""
+    period_ticks = 160                       # 16 s loop per stream, distinct per stream
+    P = period_ticks * 1600
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed + 7)
+    rng = np.random.Generator(np.random.PCG64(seed + 11))
+    sig = torch.from_numpy(rng.uniform(1e-4, 3e-3, n_streams).astype(np.float32)).to(dev)
+    pcm = torch.randn((n_streams, P), generator=g, device=dev, dtype=torch.float32) * sig[:, None]
+    wv = torch.from_numpy(word).to(dev)
+    wl = len(word)
+    # five events per 16 s loop per stream at jittered positions: words and distractors
+    for e in range(5):
+        pos = (e * P // 5 + rng.integers(0, 8000, n_streams)).astype(np.int64)
+        gain = torch.from_numpy(rng.uniform(0.3, 2.0, n_streams).astype(np.float32)).to(dev)
+        rev = torch.from_numpy(rng.random(n_streams) < 0.3).to(dev)
+        src = torch.where(rev[:, None], wv.flip(0)[None, :], wv[None, :]) * gain[:, None]
+        idx = torch.from_numpy(pos).to(dev)[:, None] + torch.arange(wl, device=dev)[None, :]
+        pcm.scatter_add_(1, idx, src)
+    torch.cuda.synchronize()
+    se = eng_mod.StreamEngine(n_streams, gpu=dev.index if dev.index is not None else 0)
+    se.template_from_pcm(word)
+    stride = P
+    base = pcm.data_ptr()
+
+    def run(t0, nt, per_call):
+        t = t0
+        while t < t0 + nt:
+            k = t % period_ticks
+            n = min(per_call, nt - (t - t0), period_ticks - k)
+            se.push_device(base + k * 1600 * 4, stride, 1600, n)
+            t += n
+        return t
+
+    t = run(0, 100, 32)                      # prefill (ring fill + detection start)
+    se.sync()
+    se.poll()
+    se.profile(True)
+    torch.cuda.synchronize()
+    w0 = time.perf_counter()
+    t = run(t, n_ticks, 1)
+    se.sync()
+    wall = time.perf_counter() - w0
+    gate_ms, gate_n = se.profile_read(2)
+    sc_ms, sc_n = se.profile_read(0)
+    r_ms, r_n = se.profile_read(1)
+    ev = se.poll(cap=64 * n_streams)
+    per_tick = wall / n_ticks
+    real = ev[(ev["flags"] & 1) == 0]
+    out = {"streams": n_streams, "ticks": n_ticks, "audio_seconds_per_stream": n_ticks * 0.1,
+           "wall_s": wall, "ms_per_tick": per_tick * 1e3,
+           "realtime_factor": 0.1 / per_tick,
+           "streams_realtime": n_streams * 0.1 / per_tick,
+           "gate_kernel_ms_per_tick": gate_ms / max(1, gate_n),
+           "scorer_kernel_ms_per_tick": (sc_ms + r_ms) / max(1, sc_n),
+           "events": int(len(real)), "matches": int(real["match"].sum()) if len(real) else 0,
+           "mfcc_frames": int((1 + real["length"].astype(np.int64) // HOP).sum()) if len(real) else 0}
+    se.close()
+    del pcm
+    return out
+
+
+# --------------------------------------------------------------------------- main
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import easywakeword_amd as ewa
+    word = load_word()
+    n_seg = args.streams * args.segments_per_stream
+    pcm, d_off, d_len, frames, lengths, offsets = make_segments(torch, dev, n_seg, args.seed + 1000 * rank, word)
+    mean = torch.empty((n_seg, 20), device=dev, dtype=torch.float32)
+    std = torch.empty((n_seg, 20), device=dev, dtype=torch.float32)
+    score = torch.empty(n_seg, device=dev, dtype=torch.float64)
+    match = torch.empty(n_seg, device=dev, dtype=torch.uint8)
+    eng = ewa.Engine(gpu=local)
+    eng.template_from_pcm(word)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    if world > 1:
+        g_score = [torch.empty_like(score) for _ in range(world)]
+        g_match = [torch.empty_like(match) for _ in range(world)]
+
+    def step():
+        eng.score_device(pcm.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n_seg, mean.data_ptr(),
+                         std.data_ptr(), score.data_ptr(), match.data_ptr(), sh)
+        if world > 1:   # gather every rank's decisions to all (rank 0 runs the confirm stage)
+            dist.all_gather(g_score, score)
+            dist.all_gather(g_match, match)
+
+    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.profile(True)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    k_ms, k_n = eng.profile_read(0)
+    r_ms, r_n = eng.profile_read(1)
+    eng.profile(False)
+    step_ms = ev0.elapsed_time(ev1) / args.steps
+    t_rank = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t_rank, op=dist.ReduceOp.MAX)
+    t_max = float(t_rank.item())
+    value = frames * world * args.steps / t_max
+    n_match = int(match.sum().item())
+    n_nan = int(torch.isnan(score).sum().item())
+
+    kernel_s = (k_ms / max(1, k_n)) / 1e3
+    achieved = frames * BYTES_PER_FRAME / kernel_s / 1e9
+
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": t_max / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (ragged segments built from tests/golden/reference_word.wav + Gaussian noise, seeded)",
+        "config": {
+            "workload": f"configs[1]: {args.streams} streams x {args.segments_per_stream} gated segments per GPU "
+                        f"(L~U{{6400..33600}}), MFCC(20,512,160)+cosine match per segment",
+            "segments_per_gpu": n_seg,
+            "frames_per_step_per_gpu": frames,
+            "global_batch": n_seg * world,
+            "parallelism": f"dp{world} (stream shards, RCCL all-gather of decisions)" if world > 1 else "dp1",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_score_f32",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel_ms": kernel_s * 1e3,
+            "launches": k_n,
+            "algorithmic_bytes_per_launch": frames * BYTES_PER_FRAME,
+        },
+        "step_event_ms": step_ms,
+        "rescore_kernel_ms": r_ms / max(1, r_n),
+        "matches_per_step": n_match,
+        "nan_scores": n_nan,
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sample = min(n_seg, 16 * 400)
+        host = pcm[: int(offsets[sample - 1] + lengths[sample - 1])].cpu().numpy()
+        out["cpu_baseline"] = cpu_baseline(host, lengths[:sample], offsets[:sample], args.cpu_seconds)
+    if not args.no_streaming:
+        del pcm
+        torch.cuda.empty_cache()
+        st = streaming_bench(torch, dev, ewa, args.stream_count, args.stream_ticks, args.seed + rank, word)
+        out["streaming"] = st
+        tot = torch.tensor([st["streams_realtime"]], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(tot)
+        out["streams_realtime_total"] = float(tot.item())
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

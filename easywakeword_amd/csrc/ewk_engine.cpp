@@ -1,0 +1,721 @@
+// ewk_engine.cpp -- the C ABI (include/ewk.h): engine lifetime, device memory,
+// the level-2 batch scorer entry points and the level-1+2 streaming tick path.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "ewk_gate.h"
+#include "ewk_internal.h"
+
+using namespace ewk;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess)                                                                  \
+            return fail(EWK_EHIP, std::string(#expr) + ": " + hipGetErrorString(_e));          \
+    } while (0)
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;   // elements
+    hipError_t reserve(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e == hipSuccess) cap = n;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace
+
+struct ewk_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    ewk_config cfg{};
+    int32_t n_streams = 0;
+    int64_t ring_len = 0;
+    int32_t n_blocks = 0;
+    int64_t n_last = 0;
+
+    Tables* d_tab = nullptr;
+    Tables64* d_tab64 = nullptr;
+    float* d_tmpl = nullptr;
+    float h_tmpl[2 * NMFCC];
+    bool has_tmpl = false;
+
+    // rescoring
+    int32_t* d_rescore = nullptr;   // [0] = count, [1..] list
+    int32_t* d_work = nullptr;      // scorer work counter
+    int32_t rescore_cap = 4096;
+    DevBuf<double> f64_scratch;
+    int f64_grid = 64;
+
+    // host-API staging
+    DevBuf<float> pcm;
+    DevBuf<int64_t> offsets;
+    DevBuf<int32_t> lengths;
+    DevBuf<float> mean, stdv;
+    DevBuf<double> score;
+    DevBuf<uint8_t> match;
+    DevBuf<double> mean64, std64;
+
+    // streaming
+    float* d_ring = nullptr;
+    double* d_brms = nullptr;
+    GateStream* d_st = nullptr;
+    ewk_event* d_events = nullptr;
+    int32_t* d_evc = nullptr;   // [0] count, [1] dropped, [2] scored watermark
+    int32_t ev_cap = 0;
+    DevBuf<float> push_stage;
+    int64_t tick = 0;
+    int32_t lds_gate = 0;
+
+    // measurement: (start, stop) event pairs per kernel family
+    bool prof = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[3];
+    std::vector<hipEvent_t> ev_pool;
+};
+
+static hipEvent_t pool_event(ewk_engine* e) {
+    if (!e->ev_pool.empty()) {
+        hipEvent_t x = e->ev_pool.back();
+        e->ev_pool.pop_back();
+        return x;
+    }
+    hipEvent_t x = nullptr;
+    if (hipEventCreate(&x) != hipSuccess) return nullptr;
+    return x;
+}
+
+// RAII bracket: records start/stop events around one launch when profiling.
+struct ProfScope {
+    ewk_engine* e;
+    int kind;
+    hipStream_t s;
+    hipEvent_t a = nullptr, b = nullptr;
+    ProfScope(ewk_engine* e_, int kind_, hipStream_t s_) : e(e_), kind(kind_), s(s_) {
+        if (!e->prof) return;
+        a = pool_event(e);
+        b = pool_event(e);
+        if (a) (void)hipEventRecord(a, s);
+    }
+    ~ProfScope() {
+        if (!e->prof || !a || !b) return;
+        (void)hipEventRecord(b, s);
+        e->ev[kind].push_back({a, b});
+    }
+};
+
+static void zero_event_state(ewk_engine* e) {
+    if (e->d_evc) (void)hipMemsetAsync(e->d_evc, 0, 4 * sizeof(int32_t), e->stream);
+}
+
+extern "C" {
+
+void ewk_default_config(ewk_config* c) {
+    memset(c, 0, sizeof(*c));
+    c->sample_rate = 16000;
+    c->buffer_seconds = 10;
+    c->block = 1600;
+    c->tick_seconds = 0.1;
+    c->pre_speech_silence = 0.8;
+    c->speech_duration_min = 0.3;
+    c->speech_duration_max = 2.0;
+    c->post_speech_silence = 0.4;
+    c->padding = 0.05;
+    c->max_segment_seconds = 3.0;
+    c->similarity_threshold = 75.0;
+    c->reentry_timeout = 0.0;
+    c->min_threshold = 0.005;
+    c->initial_threshold = 0.01;
+    c->rescore_margin = 1e-3;
+}
+
+const char* ewk_last_error(void) { return g_err.c_str(); }
+int ewk_abi_version(void) { return EWK_ABI_VERSION; }
+
+int ewk_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void ewk_destroy(ewk_engine* e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    if (e->stream) (void)hipStreamSynchronize(e->stream);
+    (void)hipFree(e->d_tab);
+    (void)hipFree(e->d_tab64);
+    (void)hipFree(e->d_tmpl);
+    (void)hipFree(e->d_rescore);
+    (void)hipFree(e->d_work);
+    e->f64_scratch.release();
+    e->pcm.release();
+    e->offsets.release();
+    e->lengths.release();
+    e->mean.release();
+    e->stdv.release();
+    e->score.release();
+    e->match.release();
+    e->mean64.release();
+    e->std64.release();
+    e->push_stage.release();
+    (void)hipFree(e->d_ring);
+    (void)hipFree(e->d_brms);
+    (void)hipFree(e->d_st);
+    (void)hipFree(e->d_events);
+    (void)hipFree(e->d_evc);
+    if (e->stream) (void)hipStreamDestroy(e->stream);
+    delete e;
+}
+
+int ewk_reset_streams(ewk_engine* e);
+
+int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config* cfg) {
+    if (!out) return fail(EWK_EINVAL, "out is NULL");
+    *out = nullptr;
+    ewk_config c;
+    if (cfg) c = *cfg;
+    else ewk_default_config(&c);
+    if (c.sample_rate != 16000) return fail(EWK_EINVAL, "sample_rate must be 16000 (SoundBuffer.FREQUENCY)");
+    if (c.buffer_seconds <= 0) return fail(EWK_EINVAL, "buffer_seconds must be positive");
+    if (c.block <= 0 || c.block > 8192) return fail(EWK_EINVAL, "block must be in [1, 8192]");
+    if (c.tick_seconds <= 0) return fail(EWK_EINVAL, "tick_seconds must be positive");
+    if (c.pre_speech_silence <= 0) return fail(EWK_EINVAL, "pre_speech_silence must be positive");
+    if (c.speech_duration_min <= 0) return fail(EWK_EINVAL, "speech_duration_min must be positive");
+    if (c.speech_duration_max <= 0) return fail(EWK_EINVAL, "speech_duration_max must be positive");
+    if (c.speech_duration_min > c.speech_duration_max)
+        return fail(EWK_EINVAL, "speech_duration_min must be <= speech_duration_max");
+    if (c.post_speech_silence <= 0) return fail(EWK_EINVAL, "post_speech_silence must be positive");
+    if (n_streams < 0) return fail(EWK_EINVAL, "n_streams must be >= 0");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(EWK_ENODEV, "no HIP device visible");
+    if (device < 0 || device >= ndev) return fail(EWK_ENODEV, "device index out of range");
+    HIP_TRY(hipSetDevice(device));
+
+    ewk_engine* e = new ewk_engine();
+    e->device = device;
+    e->cfg = c;
+    e->n_streams = n_streams;
+    e->ring_len = (int64_t)c.buffer_seconds * c.sample_rate;
+    e->n_blocks = (int32_t)(e->ring_len / c.block);
+    e->n_last = (int64_t)(0.1 * (double)c.sample_rate);   // int(0.1 * FREQUENCY)
+    auto bail = [&](hipError_t err, const char* what) {
+        std::string m = std::string(what) + ": " + hipGetErrorString(err);
+        ewk_destroy(e);
+        return fail(err == hipErrorOutOfMemory ? EWK_ENOMEM : EWK_EHIP, m);
+    };
+    hipError_t err;
+    if ((err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking)) != hipSuccess) return bail(err, "stream");
+    {
+        std::vector<unsigned char> buf(sizeof(Tables));
+        Tables* t = reinterpret_cast<Tables*>(buf.data());
+        build_tables(t);
+        if (t->melw_count > MELW_CAP) {
+            ewk_destroy(e);
+            return fail(EWK_EHIP, "mel table overflow");
+        }
+        if ((err = hipMalloc(&e->d_tab, sizeof(Tables))) != hipSuccess) return bail(err, "tables");
+        if ((err = hipMemcpy(e->d_tab, t, sizeof(Tables), hipMemcpyHostToDevice)) != hipSuccess) return bail(err, "tables");
+        std::vector<unsigned char> buf64(sizeof(Tables64));
+        Tables64* t64 = reinterpret_cast<Tables64*>(buf64.data());
+        build_tables64(t64);
+        if ((err = hipMalloc(&e->d_tab64, sizeof(Tables64))) != hipSuccess) return bail(err, "tables64");
+        if ((err = hipMemcpy(e->d_tab64, t64, sizeof(Tables64), hipMemcpyHostToDevice)) != hipSuccess)
+            return bail(err, "tables64");
+    }
+    if ((err = hipMalloc(&e->d_tmpl, 2 * NMFCC * sizeof(float))) != hipSuccess) return bail(err, "template");
+    if ((err = hipMalloc(&e->d_rescore, (1 + e->rescore_cap) * sizeof(int32_t))) != hipSuccess)
+        return bail(err, "rescore");
+    if ((err = hipMalloc(&e->d_work, 4 * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
+    // fp64 scratch: log-mel + mfcc rows for the longest ring segment
+    {
+        const int64_t tmax = 1 + e->ring_len / HOP;
+        const int64_t per = tmax * (NMEL + NMFCC);
+        if ((err = e->f64_scratch.reserve((size_t)per * e->f64_grid)) != hipSuccess) return bail(err, "f64 scratch");
+    }
+    if (n_streams > 0) {
+        const size_t ring_bytes = (size_t)n_streams * e->ring_len * sizeof(float);
+        if ((err = hipMalloc(&e->d_ring, ring_bytes)) != hipSuccess) return bail(err, "ring");
+        if ((err = hipMalloc(&e->d_brms, (size_t)n_streams * std::max(1, e->n_blocks) * sizeof(double))) != hipSuccess)
+            return bail(err, "block rms");
+        if ((err = hipMalloc(&e->d_st, (size_t)n_streams * sizeof(GateStream))) != hipSuccess) return bail(err, "state");
+        e->ev_cap = std::max(4096, 4 * n_streams);
+        if ((err = hipMalloc(&e->d_events, (size_t)e->ev_cap * sizeof(ewk_event))) != hipSuccess)
+            return bail(err, "events");
+        if ((err = hipMalloc(&e->d_evc, 4 * sizeof(int32_t))) != hipSuccess) return bail(err, "event counters");
+        e->lds_gate = gate_lds_per_wave(e->n_blocks);
+        int rc = ewk_reset_streams(e);
+        if (rc != EWK_OK) {
+            std::string m = g_err;
+            ewk_destroy(e);
+            return fail(rc, m);
+        }
+    }
+    if ((err = hipStreamSynchronize(e->stream)) != hipSuccess) return bail(err, "sync");
+    *out = e;
+    return EWK_OK;
+}
+
+int ewk_sync(ewk_engine* e) {
+    if (!e) return fail(EWK_EINVAL, "engine is NULL");
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return EWK_OK;
+}
+
+void* ewk_stream_handle(ewk_engine* e) { return e ? (void*)e->stream : nullptr; }
+
+int ewk_set_template(ewk_engine* e, const float* mean20, const float* std20) {
+    if (!e || !mean20 || !std20) return fail(EWK_EINVAL, "NULL argument");
+    memcpy(e->h_tmpl, mean20, NMFCC * sizeof(float));
+    memcpy(e->h_tmpl + NMFCC, std20, NMFCC * sizeof(float));
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipMemcpyAsync(e->d_tmpl, e->h_tmpl, sizeof(e->h_tmpl), hipMemcpyHostToDevice, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    e->has_tmpl = true;
+    return EWK_OK;
+}
+
+int ewk_set_similarity_threshold(ewk_engine* e, double threshold) {
+    if (!e) return fail(EWK_EINVAL, "engine is NULL");
+    if (!(threshold == threshold)) return fail(EWK_EINVAL, "threshold is NaN");
+    e->cfg.similarity_threshold = threshold;
+    return EWK_OK;
+}
+
+int ewk_get_template(ewk_engine* e, float* mean20, float* std20) {
+    if (!e) return fail(EWK_EINVAL, "engine is NULL");
+    if (!e->has_tmpl) return fail(EWK_ENOTEMPLATE, "No reference word set. Call set_reference() first.");
+    if (mean20) memcpy(mean20, e->h_tmpl, NMFCC * sizeof(float));
+    if (std20) memcpy(std20, e->h_tmpl + NMFCC, NMFCC * sizeof(float));
+    return EWK_OK;
+}
+
+static ScoreArgs base_args(ewk_engine* e) {
+    ScoreArgs a;
+    memset(&a, 0, sizeof(a));
+    a.has_template = e->has_tmpl ? 1 : 0;
+    a.tmpl = e->d_tmpl;
+    a.threshold = e->cfg.similarity_threshold;
+    a.rescore_margin = e->cfg.rescore_margin;
+    a.rescore_count = e->d_rescore;
+    a.rescore_list = e->d_rescore + 1;
+    a.rescore_cap = e->rescore_cap;
+    a.work = e->d_work;
+    return a;
+}
+
+// f32 scorer + fp64 rescoring of the near-threshold list, all on `s`.
+static int score_linear(ewk_engine* e, const float* d_pcm, const int64_t* d_off, const int32_t* d_len, int32_t n,
+                        float* d_mean, float* d_std, double* d_score, uint8_t* d_match, hipStream_t s) {
+    ScoreArgs a = base_args(e);
+    a.pcm = d_pcm;
+    a.offsets = d_off;
+    a.lengths = d_len;
+    a.n_seg = n;
+    a.out_mean = d_mean;
+    a.out_std = d_std;
+    a.out_score = d_score;
+    a.out_match = d_match;
+    if (!a.has_template) a.rescore_list = nullptr;
+    HIP_TRY(hipMemsetAsync(e->d_rescore, 0, sizeof(int32_t), s));
+    {
+        ProfScope ps(e, 0, s);
+        HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));
+    }
+    if (a.has_template) {
+        const int64_t per = (1 + e->ring_len / HOP) * (NMEL + NMFCC);
+        ProfScope ps(e, 1, s);
+        HIP_TRY(launch_score_f64(e->d_tab64, a, 0, e->f64_scratch.p, per, e->f64_grid, nullptr, nullptr, s));
+    }
+    return EWK_OK;
+}
+
+int ewk_score_segments_device(ewk_engine* e, const float* d_pcm, const int64_t* d_offsets, const int32_t* d_lengths,
+                              int32_t n_seg, float* d_mean, float* d_std, double* d_score, uint8_t* d_match,
+                              void* stream) {
+    if (!e) return fail(EWK_EINVAL, "engine is NULL");
+    if (n_seg < 0) return fail(EWK_EINVAL, "n_seg must be >= 0");
+    if (n_seg == 0) return EWK_OK;
+    if (!d_pcm || !d_offsets || !d_lengths) return fail(EWK_EINVAL, "NULL device pointer");
+    if (e->has_tmpl && !d_score) return fail(EWK_EINVAL, "d_score is required when a template is set");
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    return score_linear(e, d_pcm, d_offsets, d_lengths, n_seg, d_mean, d_std, d_score, d_match, s);
+}
+
+static int check_segments(const int64_t* offsets, const int32_t* lengths, int32_t n_seg, int64_t n_pcm,
+                          int32_t* max_len) {
+    int32_t mx = 0;
+    for (int32_t i = 0; i < n_seg; ++i) {
+        if (lengths[i] < 0 || offsets[i] < 0 || offsets[i] + lengths[i] > n_pcm)
+            return fail(EWK_EINVAL, "segment " + std::to_string(i) + " out of range of pcm");
+        mx = std::max(mx, lengths[i]);
+    }
+    *max_len = mx;
+    return EWK_OK;
+}
+
+int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int64_t* offsets,
+                       const int32_t* lengths, int32_t n_seg, float* out_mean, float* out_std, double* out_score,
+                       uint8_t* out_match, int32_t require_template) {
+    if (!e) return fail(EWK_EINVAL, "engine is NULL");
+    if (n_seg < 0 || n_pcm < 0) return fail(EWK_EINVAL, "negative size");
+    if (require_template && !e->has_tmpl)
+        return fail(EWK_ENOTEMPLATE, "No reference word set. Call set_reference() first.");
+    if (n_seg == 0) return EWK_OK;
+    if (!offsets || !lengths || (n_pcm > 0 && !pcm)) return fail(EWK_EINVAL, "NULL argument");
+    int32_t max_len = 0;
+    int rc = check_segments(offsets, lengths, n_seg, n_pcm, &max_len);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(e->device));
+    // grow the fp64 scratch when a host batch holds longer segments than the ring
+    {
+        const int64_t tmax = std::max<int64_t>(1 + e->ring_len / HOP, 1 + max_len / HOP);
+        const int64_t per = tmax * (NMEL + NMFCC);
+        HIP_TRY(hipStreamSynchronize(e->stream));
+        HIP_TRY(e->f64_scratch.reserve((size_t)per * e->f64_grid));
+    }
+    HIP_TRY(e->pcm.reserve(std::max<int64_t>(n_pcm, 1)));
+    HIP_TRY(e->offsets.reserve(n_seg));
+    HIP_TRY(e->lengths.reserve(n_seg));
+    HIP_TRY(e->mean.reserve((size_t)n_seg * NMFCC));
+    HIP_TRY(e->stdv.reserve((size_t)n_seg * NMFCC));
+    HIP_TRY(e->score.reserve(n_seg));
+    HIP_TRY(e->match.reserve(n_seg));
+    hipStream_t s = e->stream;
+    if (n_pcm > 0) HIP_TRY(hipMemcpyAsync(e->pcm.p, pcm, n_pcm * sizeof(float), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->offsets.p, offsets, n_seg * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->lengths.p, lengths, n_seg * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    {
+        ScoreArgs a = base_args(e);
+        a.pcm = e->pcm.p;
+        a.offsets = e->offsets.p;
+        a.lengths = e->lengths.p;
+        a.n_seg = n_seg;
+        a.out_mean = e->mean.p;
+        a.out_std = e->stdv.p;
+        a.out_score = e->score.p;
+        a.out_match = e->match.p;
+        if (!a.has_template) a.rescore_list = nullptr;
+        HIP_TRY(hipMemsetAsync(e->d_rescore, 0, sizeof(int32_t), s));
+        HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));
+        if (a.has_template) {
+            const int64_t tmax = std::max<int64_t>(1 + e->ring_len / HOP, 1 + max_len / HOP);
+            HIP_TRY(launch_score_f64(e->d_tab64, a, 0, e->f64_scratch.p, tmax * (NMEL + NMFCC), e->f64_grid,
+                                     nullptr, nullptr, s));
+        }
+    }
+    if (out_mean) HIP_TRY(hipMemcpyAsync(out_mean, e->mean.p, (size_t)n_seg * NMFCC * 4, hipMemcpyDeviceToHost, s));
+    if (out_std) HIP_TRY(hipMemcpyAsync(out_std, e->stdv.p, (size_t)n_seg * NMFCC * 4, hipMemcpyDeviceToHost, s));
+    if (e->has_tmpl) {
+        if (out_score) HIP_TRY(hipMemcpyAsync(out_score, e->score.p, n_seg * sizeof(double), hipMemcpyDeviceToHost, s));
+        if (out_match) HIP_TRY(hipMemcpyAsync(out_match, e->match.p, n_seg, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    return EWK_OK;
+}
+
+int ewk_score_segments_f64(ewk_engine* e, const float* pcm, int64_t n_pcm, const int64_t* offsets,
+                           const int32_t* lengths, int32_t n_seg, double* out_mean, double* out_std,
+                           double* out_score) {
+    if (!e) return fail(EWK_EINVAL, "engine is NULL");
+    if (n_seg < 0 || n_pcm < 0) return fail(EWK_EINVAL, "negative size");
+    if (n_seg == 0) return EWK_OK;
+    if (!offsets || !lengths || (n_pcm > 0 && !pcm)) return fail(EWK_EINVAL, "NULL argument");
+    int32_t max_len = 0;
+    int rc = check_segments(offsets, lengths, n_seg, n_pcm, &max_len);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = e->stream;
+    const int64_t tmax = std::max<int64_t>(1 + e->ring_len / HOP, 1 + max_len / HOP);
+    const int64_t per = tmax * (NMEL + NMFCC);
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(e->f64_scratch.reserve((size_t)per * e->f64_grid));
+    HIP_TRY(e->pcm.reserve(std::max<int64_t>(n_pcm, 1)));
+    HIP_TRY(e->offsets.reserve(n_seg));
+    HIP_TRY(e->lengths.reserve(n_seg));
+    HIP_TRY(e->mean64.reserve((size_t)n_seg * NMFCC));
+    HIP_TRY(e->std64.reserve((size_t)n_seg * NMFCC));
+    HIP_TRY(e->score.reserve(n_seg));
+    if (n_pcm > 0) HIP_TRY(hipMemcpyAsync(e->pcm.p, pcm, n_pcm * sizeof(float), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->offsets.p, offsets, n_seg * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(e->lengths.p, lengths, n_seg * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    ScoreArgs a = base_args(e);
+    a.pcm = e->pcm.p;
+    a.offsets = e->offsets.p;
+    a.lengths = e->lengths.p;
+    a.n_seg = n_seg;
+    a.out_score = e->score.p;
+    a.rescore_list = nullptr;
+    a.rescore_count = nullptr;
+    HIP_TRY(launch_score_f64(e->d_tab64, a, 0, e->f64_scratch.p, per, e->f64_grid, e->mean64.p, e->std64.p, s));
+    if (out_mean) HIP_TRY(hipMemcpyAsync(out_mean, e->mean64.p, (size_t)n_seg * NMFCC * 8, hipMemcpyDeviceToHost, s));
+    if (out_std) HIP_TRY(hipMemcpyAsync(out_std, e->std64.p, (size_t)n_seg * NMFCC * 8, hipMemcpyDeviceToHost, s));
+    if (out_score && e->has_tmpl)
+        HIP_TRY(hipMemcpyAsync(out_score, e->score.p, n_seg * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return EWK_OK;
+}
+
+int ewk_template_from_pcm(ewk_engine* e, const float* pcm, int64_t n) {
+    if (!e || (!pcm && n > 0)) return fail(EWK_EINVAL, "NULL argument");
+    if (n <= 0 || n > INT32_MAX) return fail(EWK_EINVAL, "template length must be in [1, 2^31)");
+    const int64_t off = 0;
+    const int32_t len = (int32_t)n;
+    float m[NMFCC], sd[NMFCC];
+    const bool had = e->has_tmpl;
+    e->has_tmpl = false;   // compute stats only
+    int rc = ewk_score_segments(e, pcm, n, &off, &len, 1, m, sd, nullptr, nullptr, 0);
+    e->has_tmpl = had;
+    if (rc) return rc;
+    return ewk_set_template(e, m, sd);
+}
+
+// ---------------------------------------------------------------- streaming path
+int ewk_reset_streams(ewk_engine* e) {
+    if (!e) return fail(EWK_EINVAL, "engine is NULL");
+    if (e->n_streams <= 0) return EWK_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = e->stream;
+    HIP_TRY(hipMemsetAsync(e->d_ring, 0, (size_t)e->n_streams * e->ring_len * sizeof(float), s));
+    HIP_TRY(hipMemsetAsync(e->d_brms, 0, (size_t)e->n_streams * std::max(1, e->n_blocks) * sizeof(double), s));
+    std::vector<GateStream> st(e->n_streams);
+    for (auto& x : st) {
+        memset(&x, 0, sizeof(x));
+        x.threshold = e->cfg.initial_threshold;
+        x.last_silent = 1;
+    }
+    HIP_TRY(hipMemcpyAsync(e->d_st, st.data(), st.size() * sizeof(GateStream), hipMemcpyHostToDevice, s));
+    zero_event_state(e);
+    HIP_TRY(hipStreamSynchronize(s));
+    e->tick = 0;
+    return EWK_OK;
+}
+
+// Score the events queued since the last scoring pass (ring mode), then advance the watermark.
+static int score_pending(ewk_engine* e) {
+    if (!e->has_tmpl) return EWK_OK;   // events keep NaN scores until a template exists
+    ScoreArgs a = base_args(e);
+    a.pcm = e->d_ring;
+    a.ring_len = e->ring_len;
+    a.events = e->d_events;
+    a.n_events = e->d_evc;
+    a.ev_base = e->d_evc + 2;
+    a.n_seg = e->ev_cap;
+    HIP_TRY(hipMemsetAsync(e->d_rescore, 0, sizeof(int32_t), e->stream));
+    {
+        ProfScope ps(e, 0, e->stream);
+        HIP_TRY(launch_score_f32(e->d_tab, a, 1, e->stream));
+    }
+    const int64_t per = (1 + e->ring_len / HOP) * (NMEL + NMFCC);
+    {
+        ProfScope ps(e, 1, e->stream);
+        HIP_TRY(launch_score_f64(e->d_tab64, a, 1, e->f64_scratch.p, per, e->f64_grid, nullptr, nullptr, e->stream));
+    }
+    HIP_TRY(launch_advance_watermark(e->d_evc + 2, e->d_evc, e->stream));
+    return EWK_OK;
+}
+
+static int push_impl(ewk_engine* e, const float* pcm, int64_t stride, int64_t tick_stride, int32_t n_ticks,
+                     int32_t flags) {
+    if (!e) return fail(EWK_EINVAL, "engine is NULL");
+    if (e->n_streams <= 0) return fail(EWK_EINVAL, "engine has no streams");
+    if (!pcm) return fail(EWK_EINVAL, "pcm is NULL");
+    if (n_ticks <= 0) return fail(EWK_EINVAL, "n_ticks must be positive");
+    if (stride < e->cfg.block && e->n_streams > 1) return fail(EWK_EINVAL, "stride must be >= block");
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = e->stream;
+    const float* src = pcm;
+    int64_t st_stride = stride, tk_stride = tick_stride;
+    if (!(flags & EWK_PUSH_DEVICE)) {
+        const size_t per_stream = (size_t)n_ticks * e->cfg.block;
+        HIP_TRY(e->push_stage.reserve(per_stream * e->n_streams));
+        for (int32_t t = 0; t < n_ticks; ++t)
+            HIP_TRY(hipMemcpy2DAsync(e->push_stage.p + (size_t)t * e->cfg.block, per_stream * sizeof(float),
+                                     pcm + (size_t)t * tick_stride, stride * sizeof(float),
+                                     e->cfg.block * sizeof(float), e->n_streams, hipMemcpyHostToDevice, s));
+        src = e->push_stage.p;
+        st_stride = (int64_t)per_stream;
+        tk_stride = e->cfg.block;
+    }
+    // Segments must be scored before the ring overwrites them: <= 32 ticks per gate launch.
+    for (int32_t t0 = 0; t0 < n_ticks; t0 += 32) {
+        const int32_t nt = std::min<int32_t>(32, n_ticks - t0);
+        GateArgs g;
+        memset(&g, 0, sizeof(g));
+        g.pcm = src + (int64_t)t0 * tk_stride;
+        g.stride = st_stride;
+        g.tick_stride = tk_stride;
+        g.n_ticks = nt;
+        g.n_streams = e->n_streams;
+        g.tick0 = e->tick;
+        g.ring = e->d_ring;
+        g.ring_len = e->ring_len;
+        g.block_rms = e->d_brms;
+        g.st = e->d_st;
+        g.block = e->cfg.block;
+        g.n_blocks = e->n_blocks;
+        g.n_last = e->n_last;
+        g.sample_rate = e->cfg.sample_rate;
+        g.lds_per_wave = e->lds_gate;
+        g.tick_seconds = e->cfg.tick_seconds;
+        g.pre_speech_silence = e->cfg.pre_speech_silence;
+        g.speech_duration_min = e->cfg.speech_duration_min;
+        g.speech_duration_max = e->cfg.speech_duration_max;
+        g.post_speech_silence = e->cfg.post_speech_silence;
+        g.padding = e->cfg.padding;
+        g.max_segment_seconds = e->cfg.max_segment_seconds;
+        g.reentry_timeout = e->cfg.reentry_timeout;
+        g.min_threshold = e->cfg.min_threshold;
+        g.events = e->d_events;
+        g.ev_count = e->d_evc;
+        g.ev_dropped = e->d_evc + 1;
+        g.ev_cap = e->ev_cap;
+        {
+            ProfScope ps(e, 2, s);
+            HIP_TRY(launch_gate(g, s));
+        }
+        e->tick += nt;
+        int rc = score_pending(e);
+        if (rc) return rc;
+    }
+    return EWK_OK;
+}
+
+int ewk_push(ewk_engine* e, const float* pcm, int64_t stride, int32_t flags) {
+    return push_impl(e, pcm, stride, 0, 1, flags);
+}
+
+int ewk_push_many(ewk_engine* e, const float* pcm, int64_t stride, int64_t tick_stride, int32_t n_ticks,
+                  int32_t flags) {
+    return push_impl(e, pcm, stride, tick_stride, n_ticks, flags);
+}
+
+int ewk_poll(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out) {
+    if (!e || !n_out) return fail(EWK_EINVAL, "NULL argument");
+    *n_out = 0;
+    if (e->n_streams <= 0) return EWK_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    int32_t cnt[4];
+    HIP_TRY(hipMemcpyAsync(cnt, e->d_evc, sizeof(cnt), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    int32_t n = std::min(cnt[0], e->ev_cap);
+    if (cnt[1] > 0) return fail(EWK_ENOMEM, "event queue overflow: " + std::to_string(cnt[1]) + " events dropped");
+    n = std::min(n, std::max(0, cap));
+    if (n > 0 && out) {
+        HIP_TRY(hipMemcpy(out, e->d_events, (size_t)n * sizeof(ewk_event), hipMemcpyDeviceToHost));
+        // order deterministically by (tick, stream)
+        std::sort(out, out + n, [](const ewk_event& x, const ewk_event& y) {
+            return x.tick != y.tick ? x.tick < y.tick : x.stream < y.stream;
+        });
+    }
+    if (n < std::min(cnt[0], e->ev_cap)) return fail(EWK_EINVAL, "poll capacity smaller than the queued events");
+    zero_event_state(e);
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    *n_out = n;
+    return EWK_OK;
+}
+
+int ewk_get_stream_state(ewk_engine* e, int32_t stream, ewk_stream_state* out) {
+    if (!e || !out) return fail(EWK_EINVAL, "NULL argument");
+    if (stream < 0 || stream >= e->n_streams) return fail(EWK_EINVAL, "stream index out of range");
+    HIP_TRY(hipSetDevice(e->device));
+    GateStream st;
+    HIP_TRY(hipMemcpyAsync(&st, e->d_st + stream, sizeof(st), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    out->samples_collected = st.collected;
+    out->tick = st.tick;
+    out->silence_threshold = st.threshold;
+    out->last_rms = st.last_rms;
+    out->silence_start_time = st.silence_start;
+    out->sound_start_time = st.sound_start;
+    out->sound_end_time = st.sound_end;
+    out->start_time = st.start_time;
+    out->pointer = st.pointer;
+    out->state = st.state;
+    out->started = st.started;
+    out->last_silent = st.last_silent;
+    return EWK_OK;
+}
+
+int ewk_read_segment(ewk_engine* e, int32_t stream, int64_t ring_start, int32_t length, float* out) {
+    if (!e || !out) return fail(EWK_EINVAL, "NULL argument");
+    if (stream < 0 || stream >= e->n_streams) return fail(EWK_EINVAL, "stream index out of range");
+    if (length < 0 || length > e->ring_len || ring_start < 0 || ring_start >= e->ring_len)
+        return fail(EWK_EINVAL, "segment out of range");
+    HIP_TRY(hipSetDevice(e->device));
+    const float* base = e->d_ring + (size_t)stream * e->ring_len;
+    const int64_t first = std::min<int64_t>(length, e->ring_len - ring_start);
+    HIP_TRY(hipMemcpyAsync(out, base + ring_start, first * sizeof(float), hipMemcpyDeviceToHost, e->stream));
+    if (length > first)
+        HIP_TRY(hipMemcpyAsync(out + first, base, (length - first) * sizeof(float), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return EWK_OK;
+}
+
+int ewk_read_last(ewk_engine* e, int32_t stream, int64_t n_samples, float* out, int64_t* n_out) {
+    if (!e || !out || !n_out) return fail(EWK_EINVAL, "NULL argument");
+    if (stream < 0 || stream >= e->n_streams) return fail(EWK_EINVAL, "stream index out of range");
+    ewk_stream_state st;
+    int rc = ewk_get_stream_state(e, stream, &st);
+    if (rc) return rc;
+    int64_t n = std::min<int64_t>(std::max<int64_t>(n_samples, 0), e->ring_len);
+    *n_out = n;
+    if (n == 0) return EWK_OK;
+    int64_t start = st.pointer - n;
+    if (start < 0) start += e->ring_len;
+    return ewk_read_segment(e, stream, start, (int32_t)n, out);
+}
+
+int ewk_profile_enable(ewk_engine* e, int32_t on) {
+    if (!e) return fail(EWK_EINVAL, "engine is NULL");
+    e->prof = on != 0;
+    return EWK_OK;
+}
+
+int ewk_profile_read(ewk_engine* e, int32_t kind, double* total_ms, int64_t* launches) {
+    if (!e || !total_ms || !launches) return fail(EWK_EINVAL, "NULL argument");
+    if (kind < 0 || kind > 2) return fail(EWK_EINVAL, "kind must be 0, 1 or 2");
+    HIP_TRY(hipSetDevice(e->device));
+    double tot = 0.0;
+    for (auto& p : e->ev[kind]) {
+        HIP_TRY(hipEventSynchronize(p.second));
+        float ms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&ms, p.first, p.second));
+        tot += ms;
+        e->ev_pool.push_back(p.first);
+        e->ev_pool.push_back(p.second);
+    }
+    *total_ms = tot;
+    *launches = (int64_t)e->ev[kind].size();
+    e->ev[kind].clear();
+    return EWK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,86 @@
+// ewk_internal.h -- shared constants, table layout and launch prototypes.
+// Internal to libewk.so; the public C ABI is include/ewk.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ewk.h"
+
+namespace ewk {
+
+// librosa.feature.mfcc(y, sr=16000, n_mfcc=20, n_fft=512, hop_length=160)
+// as called by WordMatcher.extract_mfcc (wakeword.py:561-563).
+constexpr int NFFT = 512;
+constexpr int HOP = 160;
+constexpr int NBIN = NFFT / 2 + 1;   // 257
+constexpr int NMEL = 128;
+constexpr int NMFCC = EWK_N_MFCC;    // 20
+constexpr int MELW_CAP = 768;        // packed non-zero Slaney weights (~520 used)
+constexpr int DCT_PITCH = 130;       // LDS row pitch of the DCT table (bank-conflict free A reads)
+constexpr int TILE_PITCH = 130;      // LDS row pitch of the per-wave log-mel tile
+constexpr int SCR_FRAME = 272;       // per-frame FFT scratch floats (16 rows x 17)
+constexpr int WAVES = 4;             // waves per workgroup in the fp32 scorer
+
+// Host-built constant tables (ewk_tables.cpp); copied to LDS by every workgroup.
+struct Tables {
+    float2 win2[256];        // (w[2n], w[2n+1]) periodic Hann, n = 0..255
+    float2 tw1[256];         // [k1*16 + j] = exp(-2*pi*i*j*k1/256)
+    float2 tw2[256];         // [k]  = (cos, sin)(2*pi*k/512) for the real-FFT untangle
+    int32_t band_lo[NMEL];   // first non-zero bin of mel band m
+    int32_t band_n[NMEL];    // number of non-zero bins of band m
+    int32_t band_off[NMEL];  // offset of band m in melw
+    float melw[MELW_CAP];    // 0.25 * librosa float32 weights (0.25 folds the untangle's 1/2 squared)
+    float dct[NMFCC * NMEL]; // DCT-II ortho rows 0..19
+    int32_t melw_count;
+    int32_t pad[3];
+};
+
+// fp64 path tables (rescoring / reference precision).
+struct Tables64 {
+    double win[NFFT];        // periodic Hann (scipy.signal.get_window('hann', 512, fftbins=True))
+    double cs[NFFT];         // cos(2*pi*n/512)
+    double sn[NFFT];         // sin(2*pi*n/512)
+    float melw_dense[NMEL * NBIN];  // librosa float32 mel basis [128][257]
+    double dct[NMFCC * NMEL];
+};
+
+void build_tables(Tables* t);
+void build_tables64(Tables64* t);
+
+// Segment sources for the scorer.
+//   linear: segment i = pcm[offsets[i] : offsets[i] + lengths[i]]
+//   ring  : event i -> ring + stream*ring_len, first sample ring_start, wrap at ring_len
+struct ScoreArgs {
+    const float* pcm;
+    const int64_t* offsets;
+    const int32_t* lengths;
+    ewk_event* events;        // ring mode: read stream/ring_start/length, write score/match/flags
+    const int32_t* n_events;  // ring mode: device-side event count
+    const int32_t* ev_base;   // ring mode: first unscored event (watermark)
+    int32_t* work;            // per-launch work counter (zeroed before the launch)
+    int64_t ring_len;
+    int32_t n_seg;            // linear mode count, ring mode capacity
+    int32_t has_template;
+    const float* tmpl;        // [40] template mean[20], std[20]
+    float* out_mean;
+    float* out_std;
+    double* out_score;
+    uint8_t* out_match;
+    double threshold;
+    double rescore_margin;
+    int32_t* rescore_list;    // indices whose fp32 score fell inside the margin
+    int32_t* rescore_count;
+    int32_t rescore_cap;
+};
+
+hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mode, hipStream_t s);
+// ring mode: *ev_base = *n_events after a scoring pass
+hipError_t launch_advance_watermark(int32_t* ev_base, const int32_t* n_events, hipStream_t s);
+constexpr int kScoreGridMax = 512;   // 2 workgroups x 256 CUs: one resident wave of the grid
+// fp64 re-score of rescore_list (device count) or of all n (list == nullptr).
+hipError_t launch_score_f64(const Tables64* d_tab64, const ScoreArgs& a, int ring_mode,
+                            double* d_scratch, int64_t scratch_per_seg, int grid,
+                            double* out_mean64, double* out_std64, hipStream_t s);
+
+}  // namespace ewk

@@ -1,0 +1,593 @@
+// ewk_mfcc.hip -- level-2 matcher: fused MFCC + cosine scorer for ragged segment
+// batches on gfx950 (CDNA4).
+//
+// Replaces WordMatcher.extract_mfcc / calculate_similarity / matches
+// (reference easywakeword/wakeword.py:544-639), i.e. librosa 0.11.0
+// feature.mfcc(n_mfcc=20, n_fft=512, hop=160) + scipy cosine + the score
+// scaling, for many segments per launch.
+//
+// Design (one wave = one segment; 4 waves per workgroup share the tables):
+//   frames  : stft(center=True, pad_mode=constant): frame t covers samples
+//             [t*160-256, t*160+256) of the segment, zero outside; T = 1+L//160.
+//   FFT     : 16 lanes per frame, 4 frames per wave-pass.  The 512-point real
+//             frame is packed as 256 complex points z[n] = x[2n] + i x[2n+1];
+//             256 = 16 x 16 four-step FFT: a register DFT16 per lane, a
+//             twiddle, an LDS transpose, a second register DFT16, then the
+//             real-FFT untangle X[k] = (Z[k]+Z*[256-k])/2 - i W512^k (Z[k]-Z*[256-k])/2.
+//   mel     : sparse Slaney filterbank from LDS (<=2 filters per bin), then
+//             10*log10(max(1e-10, .)); written to a 16-frame log-mel tile.
+//   DCT     : the only dense GEMM on the path: C[32 x 16] = D[32 x 128] . X[128 x 16]
+//             per 16-frame tile on the matrix cores (v_mfma_f32_16x16x4_f32, exact
+//             f32 fma chains), rows 20..31 zero.
+//   top_db  : power_to_db clamps at (segment max - 80 dB), a segment-global
+//             coupling.  Pass 1 assumes no clamp and tracks the log-mel max/min;
+//             if min < max-80 the segment is recomputed with the clamp (pass 2).
+//   stats   : population mean/std over frames from fp64 shifted sums
+//             (d = c - c[frame 0]) -- exact 0 std for identical frames.
+//   score   : fp64 cosine of the fp32-rounded stats against the fp32 template,
+//             0.7/0.3 blend, x100, p**1.5/10 (wakeword.py:611-625); NaN kept.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "ewk_internal.h"
+
+namespace ewk {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+// LDS carve (bytes, every offset a multiple of 16).
+constexpr int L_WIN2 = 0;
+constexpr int L_TW1 = L_WIN2 + 256 * 8;
+constexpr int L_TW2 = L_TW1 + 256 * 8;
+constexpr int L_BLO = L_TW2 + 256 * 8;
+constexpr int L_BN = L_BLO + NMEL * 4;
+constexpr int L_BOFF = L_BN + NMEL * 4;
+constexpr int L_MELW = L_BOFF + NMEL * 4;
+constexpr int L_DCT = L_MELW + MELW_CAP * 4;
+constexpr int L_SHARED_END = ((L_DCT + NMFCC * DCT_PITCH * 4) + 15) & ~15;
+constexpr int W_SCR = 0;                                  // 4 frames x 272 floats
+constexpr int W_TILE = W_SCR + 4 * SCR_FRAME * 4;         // 16 x 130 floats
+constexpr int W_MISC = W_TILE + 16 * TILE_PITCH * 4;      // 64 floats
+constexpr int W_BYTES = ((W_MISC + 64 * 4) + 15) & ~15;
+constexpr int LDS_BYTES = L_SHARED_END + WAVES * W_BYTES;
+static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU must fit");
+
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 w) {
+    return make_float2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
+}
+
+__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
+    const float2 t0 = make_float2(a0.x + a2.x, a0.y + a2.y);
+    const float2 t1 = make_float2(a0.x - a2.x, a0.y - a2.y);
+    const float2 t2 = make_float2(a1.x + a3.x, a1.y + a3.y);
+    const float2 t3 = make_float2(a1.x - a3.x, a1.y - a3.y);
+    a0 = make_float2(t0.x + t2.x, t0.y + t2.y);
+    a2 = make_float2(t0.x - t2.x, t0.y - t2.y);
+    a1 = make_float2(t1.x + t3.y, t1.y - t3.x);   // t1 - i t3
+    a3 = make_float2(t1.x - t3.y, t1.y + t3.x);   // t1 + i t3
+}
+
+// In-place radix-4x4 DFT16.  On return x[4*k1 + k2] holds X[k1 + 4*k2].
+__device__ __forceinline__ void dft16_perm(float2 (&x)[16]) {
+    constexpr float C1 = 0.92387953251128674f, S1 = 0.38268343236508978f, R2 = 0.70710678118654752f;
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) dft4(x[n2], x[4 + n2], x[8 + n2], x[12 + n2]);
+    // slot 4*k1 + n2 *= W16^(n2*k1)
+    x[4 * 1 + 1] = cmul(x[5], make_float2(C1, -S1));     // W^1
+    x[4 * 1 + 2] = cmul(x[6], make_float2(R2, -R2));     // W^2
+    x[4 * 1 + 3] = cmul(x[7], make_float2(S1, -C1));     // W^3
+    x[4 * 2 + 1] = cmul(x[9], make_float2(R2, -R2));     // W^2
+    x[4 * 2 + 2] = make_float2(x[10].y, -x[10].x);       // W^4 = -i
+    x[4 * 2 + 3] = cmul(x[11], make_float2(-R2, -R2));   // W^6
+    x[4 * 3 + 1] = cmul(x[13], make_float2(S1, -C1));    // W^3
+    x[4 * 3 + 2] = cmul(x[14], make_float2(-R2, -R2));   // W^6
+    x[4 * 3 + 3] = cmul(x[15], make_float2(-C1, S1));    // W^9
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) dft4(x[4 * k1], x[4 * k1 + 1], x[4 * k1 + 2], x[4 * k1 + 3]);
+}
+
+// Natural-order accessor of dft16_perm's output: X[k] lives in slot perm(k).
+__device__ __forceinline__ constexpr int dperm(int k) { return 4 * (k & 3) + (k >> 2); }
+
+struct SegView {
+    const float* p;   // stream ring base or linear pcm base
+    int64_t start;
+    int64_t ring;     // 0 = linear
+    int32_t len;
+};
+
+__device__ __forceinline__ float seg_sample(const SegView& v, int q) {
+    if (q < 0 || q >= v.len) return 0.0f;
+    int64_t idx = v.start + q;
+    if (v.ring && idx >= v.ring) idx -= v.ring;
+    return v.p[idx];
+}
+
+// One 4-frame pass: frames t0 + (lane>>4).  Writes rows [row0, row0+4) of the
+// log-mel tile.  Returns per-lane max/min of the valid log-mel values.
+__device__ __forceinline__ void frame_pass(const SegView& v, int t0, int T, int row0, bool clamp, float theta,
+                                           const unsigned char* smem, float* scr, float* tile,
+                                           int lane, float& vmax, float& vmin) {
+    const float2* s_win2 = reinterpret_cast<const float2*>(smem + L_WIN2);
+    const float2* s_tw1 = reinterpret_cast<const float2*>(smem + L_TW1);
+    const float2* s_tw2 = reinterpret_cast<const float2*>(smem + L_TW2);
+    const int* s_blo = reinterpret_cast<const int*>(smem + L_BLO);
+    const int* s_bn = reinterpret_cast<const int*>(smem + L_BN);
+    const int* s_boff = reinterpret_cast<const int*>(smem + L_BOFF);
+    const float* s_melw = reinterpret_cast<const float*>(smem + L_MELW);
+
+    const int f = lane >> 4, j = lane & 15;
+    const int t = t0 + f;
+    const bool valid = t < T;
+    float* sc = scr + f * SCR_FRAME;
+
+    // ---- load + window: lane j holds z[16*n1 + j] = x[32*n1+2j] + i x[32*n1+2j+1]
+    float2 a[16];
+    const int qbase = t * HOP - NFFT / 2 + 2 * j;
+#pragma unroll
+    for (int n1 = 0; n1 < 16; ++n1) {
+        const int q = qbase + 32 * n1;
+        const float x0 = seg_sample(v, q), x1 = seg_sample(v, q + 1);
+        const float2 w = s_win2[16 * n1 + j];
+        a[n1] = make_float2(x0 * w.x, x1 * w.y);
+    }
+    // ---- DFT16 over n1, twiddle W256^(j*k1)
+    dft16_perm(a);
+#pragma unroll
+    for (int k1 = 1; k1 < 16; ++k1) a[dperm(k1)] = cmul(a[dperm(k1)], s_tw1[k1 * 16 + j]);
+    // ---- transpose through LDS (real, then imaginary half): lane k1 <- A_{n2}[k1]
+    float2 b[16];
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) sc[k1 * 17 + j] = a[dperm(k1)].x;
+    lds_order();
+#pragma unroll
+    for (int n2 = 0; n2 < 16; ++n2) b[n2].x = sc[j * 17 + n2];
+    lds_order();
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) sc[k1 * 17 + j] = a[dperm(k1)].y;
+    lds_order();
+#pragma unroll
+    for (int n2 = 0; n2 < 16; ++n2) b[n2].y = sc[j * 17 + n2];
+    lds_order();
+    // ---- DFT16 over n2: Z[j + 16*k2] = b[dperm(k2)]
+    dft16_perm(b);
+    // ---- untangle: partner Z[(256-k) & 255], k = j + 16*k2
+    float2 zp[16];
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) sc[j + 16 * k2] = b[dperm(k2)].x;
+    lds_order();
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) zp[k2].x = sc[(256 - (j + 16 * k2)) & 255];
+    lds_order();
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) sc[j + 16 * k2] = b[dperm(k2)].y;
+    lds_order();
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) zp[k2].y = sc[(256 - (j + 16 * k2)) & 255];
+    lds_order();
+    // P'[k] = |2 X[k]|^2 = |A - i W512^k B|^2, A = Z[k] + conj(Zp), B = Z[k] - conj(Zp)
+    float pw[16];
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) {
+        const float2 z = b[dperm(k2)], p = zp[k2];
+        const float ar = z.x + p.x, ai = z.y - p.y;
+        const float br = z.x - p.x, bi = z.y + p.y;
+        const float2 cs = s_tw2[j + 16 * k2];
+        const float yr = ar - cs.y * br + cs.x * bi;
+        const float yi = ai - cs.y * bi - cs.x * br;
+        pw[k2] = yr * yr + yi * yi;
+    }
+    float p256 = 0.0f;
+    if (j == 0) {   // X[256] = Re Z[0] - Im Z[0]
+        const float2 z0 = b[dperm(0)];
+        const float y = 2.0f * (z0.x - z0.y);
+        p256 = y * y;
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) sc[j + 16 * k2] = pw[k2];
+    if (j == 0) sc[256] = p256;
+    lds_order();
+    // ---- mel + log: lane j computes bands m = j + 16*i of its frame
+    float* trow = tile + (row0 + f) * TILE_PITCH;
+#pragma unroll 2
+    for (int i = 0; i < 8; ++i) {
+        const int m = j + 16 * i;
+        const int lo = s_blo[m], n = s_bn[m], off = s_boff[m];
+        float acc = 0.0f;
+        for (int q = 0; q < n; ++q) acc = fmaf(s_melw[off + q], sc[lo + q], acc);
+        float db = 10.0f * log10f(fmaxf(1e-10f, acc));
+        if (valid) {
+            vmax = fmaxf(vmax, db);
+            vmin = fminf(vmin, db);
+        }
+        if (clamp) db = fmaxf(db, theta);
+        trow[m] = valid ? db : 0.0f;
+    }
+    lds_order();
+}
+
+// Whole-segment pipeline for one wave.  On return lanes with (lane&15)==0 hold
+// the fp64 sums for coefficients (16*rt + 4*(lane>>4) + r).
+__device__ void segment_stats(const SegView& v, const unsigned char* smem, float* scr, float* tile,
+                              int lane, bool clamp, float theta,
+                              double (&s1)[8], double (&s2)[8], float& vmax, float& vmin) {
+    const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
+    const int T = 1 + v.len / HOP;
+    const int ntile = (T + 15) >> 4;
+    const int col = lane & 15, h = lane >> 4;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; }
+    float cref[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cref[i] = 0.0f;
+    vmax = -INFINITY;
+    vmin = INFINITY;
+    for (int tile_i = 0; tile_i < ntile; ++tile_i) {
+#pragma unroll 1
+        for (int p = 0; p < 4; ++p)
+            frame_pass(v, tile_i * 16 + p * 4, T, p * 4, clamp, theta, smem, scr, tile, lane, vmax, vmin);
+        // DCT on the matrix cores: two 16-row tiles (rows 0..15, 16..31; 20..31 are zero)
+        floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        const float* brow = tile + col * TILE_PITCH + h;
+        const float* arow0 = s_dct + col * DCT_PITCH + h;
+        const float* arow1 = s_dct + (16 + (col & 3)) * DCT_PITCH + h;
+        const bool a1ok = col < 4;
+#pragma unroll 8
+        for (int s = 0; s < 32; ++s) {
+            const float bv = brow[4 * s];
+            const float a0 = arow0[4 * s];
+            const float a1 = a1ok ? arow1[4 * s] : 0.0f;
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bv, acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bv, acc1, 0, 0, 0);
+        }
+        lds_order();
+        // lane holds C[row = 4h + r][frame col] for both row tiles
+        float c[8] = {acc0[0], acc0[1], acc0[2], acc0[3], acc1[0], acc1[1], acc1[2], acc1[3]};
+        if (tile_i == 0) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
+        }
+        const bool fvalid = tile_i * 16 + col < T;
+        if (fvalid) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const double d = (double)c[i] - (double)cref[i];
+                s1[i] += d;
+                s2[i] = fma(d, d, s2[i]);
+            }
+        }
+    }
+    // reduce over the 16 frame columns (xor 1,2,4,8 stays inside a 16-lane row),
+    // then mean = cref + s1/T, var = (s2 - s1^2/T)/T  (returned in s1 / s2)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+        for (int m = 1; m < 16; m <<= 1) {
+            s1[i] += __shfl_xor(s1[i], m, 64);
+            s2[i] += __shfl_xor(s2[i], m, 64);
+        }
+        const double Td = (double)T;
+        const double mean = (double)cref[i] + s1[i] / Td;
+        double var = (s2[i] - s1[i] * s1[i] / Td) / Td;
+        var = var > 0.0 ? var : 0.0;
+        s1[i] = mean;
+        s2[i] = sqrt(var);
+    }
+    // wave-wide log-mel max/min
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        vmax = fmaxf(vmax, __shfl_xor(vmax, m, 64));
+        vmin = fminf(vmin, __shfl_xor(vmin, m, 64));
+    }
+}
+
+__device__ __forceinline__ double wave_sum(double x) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) x += __shfl_xor(x, m, 64);
+    return x;
+}
+
+// scipy 1.15 correlation/cosine: dist = clip(1 - uv/sqrt(uu*vv), 0, 2), NaN kept.
+__device__ __forceinline__ double cosine_dist(double uv, double uu, double vv) {
+#pragma clang fp contract(off)
+    double d = 1.0 - uv / sqrt(uu * vv);
+    if (d < 0.0) d = 0.0;
+    else if (d > 2.0) d = 2.0;
+    return d;
+}
+
+__device__ __forceinline__ double scaled_similarity(double sm, double ss) {
+#pragma clang fp contract(off)
+    const double combined = sm * 0.7 + ss * 0.3;
+    const double percent = combined * 100.0;
+    return pow(percent, 1.5) / 10.0;   // 100**0.5 == 10.0 exactly
+}
+
+template <int RING>
+__global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__ tab, ScoreArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    // ---- cooperative table load (global -> LDS)
+    {
+        const float4* g = reinterpret_cast<const float4*>(tab);
+        float4* s = reinterpret_cast<float4*>(smem);
+        // win2, tw1, tw2 are contiguous at the start of Tables (3 * 2048 B)
+        for (int i = threadIdx.x; i < 3 * 2048 / 16; i += blockDim.x) s[i] = g[i];
+        int* sb = reinterpret_cast<int*>(smem + L_BLO);
+        for (int i = threadIdx.x; i < 3 * NMEL; i += blockDim.x) sb[i] = tab->band_lo[i];  // lo,n,off contiguous
+        float* sw = reinterpret_cast<float*>(smem + L_MELW);
+        for (int i = threadIdx.x; i < MELW_CAP; i += blockDim.x) sw[i] = tab->melw[i];
+        float* sd = reinterpret_cast<float*>(smem + L_DCT);
+        for (int i = threadIdx.x; i < NMFCC * NMEL; i += blockDim.x)
+            sd[(i / NMEL) * DCT_PITCH + (i % NMEL)] = tab->dct[i];
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int base = 0, count = a.n_seg;
+    if (RING) {
+        base = *a.ev_base;
+        count = min(*a.n_events, a.n_seg) - base;
+    }
+    unsigned char* wbase = smem + L_SHARED_END + wave * W_BYTES;
+    float* scr = reinterpret_cast<float*>(wbase + W_SCR);
+    float* tile = reinterpret_cast<float*>(wbase + W_TILE);
+    float* misc = reinterpret_cast<float*>(wbase + W_MISC);
+    // persistent waves pull segments from a work counter (ragged lengths balance)
+    for (;;) {
+    int idx = 0;
+    if (lane == 0) idx = atomicAdd(a.work, 1);
+    idx = __shfl(idx, 0, 64);
+    if (idx >= count) break;
+    const int seg = base + idx;
+
+    SegView v;
+    if (RING) {
+        const ewk_event ev = a.events[seg];
+        v.p = a.pcm + (int64_t)ev.stream * a.ring_len;
+        v.start = ev.ring_start;
+        v.ring = a.ring_len;
+        v.len = ev.length;
+        if (ev.flags & EWK_EV_SKIPPED) continue;
+    } else {
+        v.p = a.pcm;
+        v.start = a.offsets[seg];
+        v.ring = 0;
+        v.len = a.lengths[seg];
+    }
+
+    double st1[8], st2[8];
+    float vmax, vmin;
+    segment_stats(v, smem, scr, tile, lane, false, 0.0f, st1, st2, vmax, vmin);
+    const float theta = vmax - 80.0f;
+    if (vmin < theta) segment_stats(v, smem, scr, tile, lane, true, theta, st1, st2, vmax, vmin);
+
+    // ---- gather fp32-rounded mean/std into misc[0..19], misc[20..39]
+    if ((lane & 15) == 0) {
+        const int h = lane >> 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            misc[4 * h + r] = (float)st1[r];
+            misc[20 + 4 * h + r] = (float)st2[r];
+            if (h == 0) {
+                misc[16 + r] = (float)st1[4 + r];
+                misc[36 + r] = (float)st2[4 + r];
+            }
+        }
+    }
+    lds_order();
+    float cm = 0.0f, cs = 0.0f;
+    if (lane < NMFCC) {
+        cm = misc[lane];
+        cs = misc[20 + lane];
+        if (!RING) {
+            if (a.out_mean) a.out_mean[(int64_t)seg * NMFCC + lane] = cm;
+            if (a.out_std) a.out_std[(int64_t)seg * NMFCC + lane] = cs;
+        }
+    }
+    if (!a.has_template) continue;
+    double tm = 0.0, ts = 0.0;
+    if (lane < NMFCC) {
+        tm = a.tmpl[lane];
+        ts = a.tmpl[NMFCC + lane];
+    }
+    const double uv_m = wave_sum(tm * (double)cm), uu_m = wave_sum(tm * tm), vv_m = wave_sum((double)cm * cm);
+    const double uv_s = wave_sum(ts * (double)cs), uu_s = wave_sum(ts * ts), vv_s = wave_sum((double)cs * cs);
+    if (lane == 0) {
+        const double sm = 1.0 - cosine_dist(uv_m, uu_m, vv_m);
+        const double ss = 1.0 - cosine_dist(uv_s, uu_s, vv_s);
+        const double score = scaled_similarity(sm, ss);
+        const int match = score >= a.threshold;
+        const bool near = fabs(score - a.threshold) < a.rescore_margin;
+        if (RING) {
+            a.events[seg].score = score;
+            a.events[seg].match = match;
+        } else {
+            a.out_score[seg] = score;
+            if (a.out_match) a.out_match[seg] = (uint8_t)match;
+        }
+        if (near && a.rescore_list) {
+            const int slot = atomicAdd(a.rescore_count, 1);
+            if (slot < a.rescore_cap) a.rescore_list[slot] = seg;
+        }
+    }
+    lds_order();
+    }   // work loop
+}
+
+__global__ void k_advance(int32_t* ev_base, const int32_t* n_events) { *ev_base = *n_events; }
+
+hipError_t launch_advance_watermark(int32_t* ev_base, const int32_t* n_events, hipStream_t s) {
+    hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, s, ev_base, n_events);
+    return hipGetLastError();
+}
+
+hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mode, hipStream_t s) {
+    if (a.n_seg <= 0) return hipSuccess;
+    const int grid = ring_mode ? 256 : min((a.n_seg + WAVES - 1) / WAVES, kScoreGridMax);
+    hipError_t e = hipMemsetAsync(a.work, 0, sizeof(int32_t), s);
+    if (e != hipSuccess) return e;
+    if (ring_mode)
+        hipLaunchKernelGGL(k_score_f32<1>, dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
+    else
+        hipLaunchKernelGGL(k_score_f32<0>, dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
+    return hipGetLastError();
+}
+
+// ============================================================================
+// fp64 reference-precision path (re-scoring near the decision threshold).
+// One 256-thread workgroup per segment; direct 512-point DFT per frame in fp64
+// with the float32-rounded librosa mel basis, fp64 log10, top_db clamp,
+// fp64 DCT and two-pass mean/std -- the float64 candidate path of the
+// reference (wakeword.py:1105-1121 hands float64 ring slices to librosa).
+// ============================================================================
+// numpy's float64 pairwise add.reduce over n strided values (n <= 8192: one ufunc buffer)
+__device__ double pw_sum(const double* a, int n, int stride) {
+    if (n < 8) {
+        double r = 0.0;
+        for (int i = 0; i < n; ++i) r += a[i * stride];
+        return r;
+    }
+    if (n <= 128) {
+        double r[8];
+        for (int j = 0; j < 8; ++j) r[j] = a[j * stride];
+        int i = 8;
+        const int lim = n - (n % 8);
+        for (; i < lim; i += 8)
+            for (int j = 0; j < 8; ++j) r[j] += a[(i + j) * stride];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; ++i) res += a[i * stride];
+        return res;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return pw_sum(a, n2, stride) + pw_sum(a + (int64_t)n2 * stride, n - n2, stride);
+}
+
+__device__ double np_sum(const double* a, int n, int stride) {
+    double acc = 0.0;
+    for (int c = 0; c < n; c += 8192) acc += pw_sum(a + (int64_t)c * stride, min(8192, n - c), stride);
+    return acc;
+}
+
+template <int RING>
+__global__ __launch_bounds__(256) void k_score_f64(const Tables64* __restrict__ tb, ScoreArgs a,
+                                                   double* scratch, int64_t per_seg,
+                                                   double* out_mean64, double* out_std64) {
+    __shared__ double s_x[NFFT];
+    __shared__ double s_p[NBIN];
+    __shared__ double s_red[256];
+    __shared__ double s_stat[2 * NMFCC];
+    const int tid = threadIdx.x;
+    int count;
+    if (a.rescore_list) count = min(*a.rescore_count, a.rescore_cap);
+    else count = RING ? min(a.n_seg, *a.n_events) : a.n_seg;
+    double* lm = scratch + (int64_t)blockIdx.x * per_seg;   // [T][128] log-mel, then [T][20] mfcc
+    for (int w = blockIdx.x; w < count; w += gridDim.x) {
+        const int seg = a.rescore_list ? a.rescore_list[w] : w;
+        SegView v;
+        if (RING) {
+            const ewk_event ev = a.events[seg];
+            v.p = a.pcm + (int64_t)ev.stream * a.ring_len;
+            v.start = ev.ring_start;
+            v.ring = a.ring_len;
+            v.len = ev.length;
+        } else {
+            v.p = a.pcm;
+            v.start = a.offsets[seg];
+            v.ring = 0;
+            v.len = a.lengths[seg];
+        }
+        const int T = 1 + v.len / HOP;
+        if ((int64_t)T * (NMEL + NMFCC) > per_seg) continue;   // host sizes scratch; never expected
+        double lmax = -INFINITY;
+        for (int t = 0; t < T; ++t) {
+            for (int n = tid; n < NFFT; n += 256) s_x[n] = tb->win[n] * (double)seg_sample(v, t * HOP - NFFT / 2 + n);
+            __syncthreads();
+            {   // bins tid (0..255) and 256 (thread 0)
+                const int k = tid;
+                double re = 0.0, im = 0.0;
+                for (int n = 0; n < NFFT; ++n) {
+                    const int idx = (n * k) & (NFFT - 1);
+                    re = fma(s_x[n], tb->cs[idx], re);
+                    im = fma(-s_x[n], tb->sn[idx], im);
+                }
+                s_p[k] = re * re + im * im;
+                if (tid == 0) {
+                    double r = 0.0;
+                    for (int n = 0; n < NFFT; ++n) r += (n & 1) ? -s_x[n] : s_x[n];
+                    s_p[256] = r * r;
+                }
+            }
+            __syncthreads();
+            if (tid < NMEL) {
+                const float* wrow = tb->melw_dense + tid * NBIN;
+                double acc = 0.0;
+                for (int k = 0; k < NBIN; ++k) acc = fma((double)wrow[k], s_p[k], acc);
+                const double db = 10.0 * log10(fmax(1e-10, acc));
+                lm[(int64_t)t * NMEL + tid] = db;
+                s_red[tid] = db;
+            }
+            __syncthreads();
+            if (tid == 0) for (int m = 0; m < NMEL; ++m) lmax = fmax(lmax, s_red[m]);
+            __syncthreads();
+        }
+        if (tid == 0) s_red[0] = lmax;
+        __syncthreads();
+        const double theta = s_red[0] - 80.0;
+        __syncthreads();
+        double* mf = lm + (int64_t)T * NMEL;
+        for (int i = tid; i < T * NMFCC; i += 256) {
+            const int t = i / NMFCC, k = i % NMFCC;
+            const double* row = lm + (int64_t)t * NMEL;
+            double acc = 0.0;
+            for (int m = 0; m < NMEL; ++m) acc = fma(tb->dct[k * NMEL + m], fmax(row[m], theta), acc);
+            mf[i] = acc;
+        }
+        __syncthreads();
+        if (tid < NMFCC) {   // np.mean / np.std(axis=1): pairwise sums, population std
+            const double mean = np_sum(mf + tid, T, NMFCC) / T;
+            for (int t = 0; t < T; ++t) { const double d = mf[t * NMFCC + tid] - mean; mf[t * NMFCC + tid] = d * d; }
+            const double sd = sqrt(np_sum(mf + tid, T, NMFCC) / T);
+            s_stat[tid] = mean;
+            s_stat[NMFCC + tid] = sd;
+            if (out_mean64) { out_mean64[(int64_t)seg * NMFCC + tid] = mean; out_std64[(int64_t)seg * NMFCC + tid] = sd; }
+        }
+        __syncthreads();
+        if (tid == 0 && a.has_template) {
+            double uvm = 0, uum = 0, vvm = 0, uvs = 0, uus = 0, vvs = 0;
+            for (int k = 0; k < NMFCC; ++k) {
+                const double tm = a.tmpl[k], ts = a.tmpl[NMFCC + k];
+                const double cm = s_stat[k], cs = s_stat[NMFCC + k];
+                uvm += tm * cm; uum += tm * tm; vvm += cm * cm;
+                uvs += ts * cs; uus += ts * ts; vvs += cs * cs;
+            }
+            const double score = scaled_similarity(1.0 - cosine_dist(uvm, uum, vvm), 1.0 - cosine_dist(uvs, uus, vvs));
+            const int match = score >= a.threshold;
+            if (RING) {
+                a.events[seg].score = score;
+                a.events[seg].match = match;
+                if (a.rescore_list) a.events[seg].flags |= EWK_EV_RESCORED;
+            } else {
+                if (a.out_score) a.out_score[seg] = score;
+                if (a.out_match) a.out_match[seg] = (uint8_t)match;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_score_f64(const Tables64* d_tab64, const ScoreArgs& a, int ring_mode, double* d_scratch,
+                            int64_t scratch_per_seg, int grid, double* out_mean64, double* out_std64,
+                            hipStream_t s) {
+    if (grid <= 0) return hipSuccess;
+    if (ring_mode)
+        hipLaunchKernelGGL(k_score_f64<1>, dim3(grid), dim3(256), 0, s, d_tab64, a, d_scratch, scratch_per_seg,
+                           out_mean64, out_std64);
+    else
+        hipLaunchKernelGGL(k_score_f64<0>, dim3(grid), dim3(256), 0, s, d_tab64, a, d_scratch, scratch_per_seg,
+                           out_mean64, out_std64);
+    return hipGetLastError();
+}
+
+}  // namespace ewk

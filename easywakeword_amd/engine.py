@@ -1,0 +1,211 @@
+"""Thin Python owners of an ``ewk_engine`` (the C ABI in include/ewk.h).
+
+``Engine``       -- scorer-only engine (level 2): the WordMatcher hot path.
+``StreamEngine`` -- N concurrent streams on one GPU (levels 1 + 2): the
+                    SoundBuffer + _detect_word hot loop for many microphones.
+
+No CPU fallback exists: construction raises when libewk.so or a GPU is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import N_MFCC, check
+
+FREQUENCY = 16000
+
+
+def _f32(audio) -> np.ndarray:
+    a = np.asarray(audio)
+    if a.ndim != 1:
+        a = a.reshape(-1)
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+class Engine:
+    """Owns one ewk_engine on `gpu` (scorer-only unless n_streams > 0)."""
+
+    def __init__(self, gpu: int = 0, n_streams: int = 0, config: Optional[_lib.EwkConfig] = None, **cfg):
+        self._lib = _lib.load()
+        self._h = C.c_void_p()
+        if config is None:
+            config = _lib.default_config(**cfg)
+        self.config = config
+        check(self._lib.ewk_create(C.byref(self._h), int(gpu), int(n_streams), C.byref(config)))
+        self.gpu = int(gpu)
+        self.n_streams = int(n_streams)
+
+    # -- lifetime ------------------------------------------------------------
+    def close(self) -> None:
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            self._lib.ewk_destroy(h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def stream_handle(self) -> int:
+        return int(self._lib.ewk_stream_handle(self._h) or 0)
+
+    def sync(self) -> None:
+        check(self._lib.ewk_sync(self._h))
+
+    # -- measurement ---------------------------------------------------------
+    def profile(self, on: bool = True) -> None:
+        check(self._lib.ewk_profile_enable(self._h, int(bool(on))))
+
+    def profile_read(self, kind: int = 0):
+        """(total_ms, launches) of the kernel family since the last read
+        (0 = fp32 scorer, 1 = fp64 re-scorer, 2 = gate)."""
+        ms = C.c_double(0.0)
+        n = C.c_int64(0)
+        check(self._lib.ewk_profile_read(self._h, int(kind), C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    # -- template ------------------------------------------------------------
+    def template_from_pcm(self, audio) -> None:
+        a = _f32(audio)
+        check(self._lib.ewk_template_from_pcm(self._h, _lib.fptr(a), len(a)))
+
+    def set_template(self, mean, std) -> None:
+        m = _f32(mean)
+        s = _f32(std)
+        if m.size != N_MFCC or s.size != N_MFCC:
+            raise ValueError(f"template must be {N_MFCC} means and {N_MFCC} stds")
+        check(self._lib.ewk_set_template(self._h, _lib.fptr(m), _lib.fptr(s)))
+
+    def get_template(self) -> Tuple[np.ndarray, np.ndarray]:
+        m = np.zeros(N_MFCC, np.float32)
+        s = np.zeros(N_MFCC, np.float32)
+        check(self._lib.ewk_get_template(self._h, _lib.fptr(m), _lib.fptr(s)))
+        return m, s
+
+    def set_threshold(self, threshold: float) -> None:
+        check(self._lib.ewk_set_similarity_threshold(self._h, float(threshold)))
+        self.config.similarity_threshold = float(threshold)
+
+    # -- level 2 over ragged host batches ------------------------------------
+    def score(self, segments, require_template: bool = True):
+        """MFCC stats + score of a list of 1-D arrays.  Returns
+        (mean[n,20] f32, std[n,20] f32, score[n] f64, match[n] bool)."""
+        segs = [_f32(s) for s in segments]
+        n = len(segs)
+        lengths = np.array([len(s) for s in segs], dtype=np.int32)
+        offsets = np.zeros(n, dtype=np.int64)
+        if n:
+            offsets[1:] = np.cumsum(lengths[:-1], dtype=np.int64)
+        pcm = np.concatenate(segs) if n else np.zeros(0, np.float32)
+        pcm = np.ascontiguousarray(pcm, dtype=np.float32)
+        return self.score_packed(pcm, offsets, lengths, require_template)
+
+    def score_packed(self, pcm: np.ndarray, offsets: np.ndarray, lengths: np.ndarray,
+                     require_template: bool = True):
+        pcm = np.ascontiguousarray(pcm, dtype=np.float32)
+        offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.int32)
+        n = len(lengths)
+        mean = np.zeros((n, N_MFCC), np.float32)
+        std = np.zeros((n, N_MFCC), np.float32)
+        score = np.full(n, np.nan, np.float64)
+        match = np.zeros(n, np.uint8)
+        check(self._lib.ewk_score_segments(self._h, _lib.fptr(pcm), len(pcm), _lib.i64ptr(offsets),
+                                           _lib.i32ptr(lengths), n, _lib.fptr(mean), _lib.fptr(std),
+                                           _lib.dptr(score), _lib.u8ptr(match), int(bool(require_template))))
+        return mean, std, score, match.astype(bool)
+
+    def score_f64(self, segments):
+        """Reference-precision (float64) path: (mean[n,20], std[n,20], score[n])."""
+        segs = [_f32(s) for s in segments]
+        n = len(segs)
+        lengths = np.array([len(s) for s in segs], dtype=np.int32)
+        offsets = np.zeros(n, dtype=np.int64)
+        if n:
+            offsets[1:] = np.cumsum(lengths[:-1], dtype=np.int64)
+        pcm = np.ascontiguousarray(np.concatenate(segs) if n else np.zeros(0, np.float32), dtype=np.float32)
+        mean = np.zeros((n, N_MFCC), np.float64)
+        std = np.zeros((n, N_MFCC), np.float64)
+        score = np.full(n, np.nan, np.float64)
+        check(self._lib.ewk_score_segments_f64(self._h, _lib.fptr(pcm), len(pcm), _lib.i64ptr(offsets),
+                                               _lib.i32ptr(lengths), n, _lib.dptr(mean), _lib.dptr(std),
+                                               _lib.dptr(score)))
+        return mean, std, score
+
+    def score_device(self, pcm_ptr: int, offsets_ptr: int, lengths_ptr: int, n: int, mean_ptr: int,
+                     std_ptr: int, score_ptr: int, match_ptr: int, stream: int = 0) -> None:
+        """Device-resident batch (e.g. torch tensor data_ptr()s); asynchronous on `stream`."""
+        check(self._lib.ewk_score_segments_device(self._h, C.c_void_p(pcm_ptr), C.c_void_p(offsets_ptr),
+                                                  C.c_void_p(lengths_ptr), int(n), C.c_void_p(mean_ptr or None),
+                                                  C.c_void_p(std_ptr or None), C.c_void_p(score_ptr or None),
+                                                  C.c_void_p(match_ptr or None), C.c_void_p(stream or None)))
+
+
+class StreamEngine(Engine):
+    """N concurrent 16 kHz streams on one GPU: ring + adaptive threshold + timing
+    FSM per stream (level 1) and MFCC matching of every gated segment (level 2)."""
+
+    def __init__(self, n_streams: int, gpu: int = 0, config: Optional[_lib.EwkConfig] = None, **cfg):
+        if n_streams <= 0:
+            raise ValueError("n_streams must be positive")
+        super().__init__(gpu=gpu, n_streams=n_streams, config=config, **cfg)
+        self.block = int(self.config.block)
+        self.ring_len = int(self.config.buffer_seconds) * FREQUENCY
+
+    def push(self, blocks: np.ndarray) -> None:
+        """One tick: `blocks` is float32 [n_streams, block] (host)."""
+        b = np.ascontiguousarray(blocks, dtype=np.float32)
+        if b.shape != (self.n_streams, self.block):
+            raise ValueError(f"expected blocks of shape {(self.n_streams, self.block)}, got {b.shape}")
+        check(self._lib.ewk_push(self._h, b.ctypes.data_as(C.c_void_p), self.block, 0))
+
+    def push_many(self, pcm: np.ndarray) -> None:
+        """Several ticks: float32 [n_streams, n_ticks * block] (host)."""
+        a = np.ascontiguousarray(pcm, dtype=np.float32)
+        if a.ndim != 2 or a.shape[0] != self.n_streams or a.shape[1] % self.block:
+            raise ValueError("pcm must be [n_streams, n_ticks*block]")
+        nt = a.shape[1] // self.block
+        if nt:
+            check(self._lib.ewk_push_many(self._h, a.ctypes.data_as(C.c_void_p), a.shape[1], self.block, nt, 0))
+
+    def push_device(self, ptr: int, stride: int, tick_stride: int = 0, n_ticks: int = 1) -> None:
+        check(self._lib.ewk_push_many(self._h, C.c_void_p(ptr), int(stride), int(tick_stride), int(n_ticks),
+                                      _lib.EWK_PUSH_DEVICE))
+
+    def poll(self, cap: Optional[int] = None) -> np.ndarray:
+        """Drain queued events as a structured array (see _lib.EVENT_DTYPE)."""
+        cap = int(cap or max(4096, 4 * self.n_streams))
+        buf = (_lib.EwkEvent * cap)()
+        n = C.c_int32(0)
+        check(self._lib.ewk_poll(self._h, buf, cap, C.byref(n)))
+        arr = np.frombuffer(buf, dtype=_lib.EVENT_DTYPE, count=n.value).copy()
+        return arr
+
+    def state(self, stream: int) -> dict:
+        st = _lib.EwkStreamState()
+        check(self._lib.ewk_get_stream_state(self._h, int(stream), C.byref(st)))
+        return {f: getattr(st, f) for f, _ in st._fields_}
+
+    def read_last(self, stream: int, n_samples: int) -> np.ndarray:
+        out = np.zeros(max(0, int(n_samples)), np.float32)
+        n = C.c_int64(0)
+        check(self._lib.ewk_read_last(self._h, int(stream), int(n_samples), _lib.fptr(out), C.byref(n)))
+        return out[: n.value]
+
+    def read_segment(self, stream: int, ring_start: int, length: int) -> np.ndarray:
+        out = np.zeros(int(length), np.float32)
+        check(self._lib.ewk_read_segment(self._h, int(stream), int(ring_start), int(length), _lib.fptr(out)))
+        return out
+
+    def reset(self) -> None:
+        check(self._lib.ewk_reset_streams(self._h))

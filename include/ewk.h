@@ -1,0 +1,178 @@
+/*
+ * ewk.h -- C ABI of the MI355X-native EasyWakeWord hot path (levels 1 + 2).
+ *
+ * The reference has no FFI; its seams are Python duck types:
+ *   - the WordMatcher protocol  (easywakeword/wakeword.py:520-639)
+ *   - the SoundBuffer protocol  (easywakeword/wakeword.py:405-517)
+ *   - the WakeWord._detect_word tick loop (easywakeword/wakeword.py:1036-1159)
+ * Each entry point below names the reference interface it replaces.  The
+ * Python facade (easywakeword_amd/wakeword.py) binds these with ctypes; the
+ * binding a maintainer would add to the reference is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *   - every int-returning call returns EWK_OK (0) or a negative EWK_E* code;
+ *     the message is in the thread-local ewk_last_error().  The facade maps
+ *     EWK_EINVAL / EWK_ENOTEMPLATE to ValueError and the rest to RuntimeError.
+ *   - the caller owns host arrays; the engine owns its device buffers and its
+ *     HIP stream.  One engine per host thread; calls are not re-entrant per
+ *     engine.
+ *   - *_device entry points take device pointers (e.g. torch tensors'
+ *     data_ptr()) and an optional hipStream_t (NULL = the engine's stream).
+ */
+#ifndef EWK_H
+#define EWK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EWK_N_MFCC 20
+#define EWK_ABI_VERSION 1
+
+#define EWK_OK 0
+#define EWK_EINVAL (-1)       /* bad parameter            -> ValueError            */
+#define EWK_ENOTEMPLATE (-2)  /* no reference word set    -> ValueError (wakeword.py:608-609) */
+#define EWK_EHIP (-3)         /* HIP runtime failure      -> RuntimeError          */
+#define EWK_ENOMEM (-4)       /* allocation failure       -> MemoryError           */
+#define EWK_ENODEV (-5)       /* no gfx950 device / bad device index -> RuntimeError */
+
+/* event flags */
+#define EWK_EV_SKIPPED 1      /* segment longer than max_segment_seconds: no level-2 call (wakeword.py:1113-1118) */
+#define EWK_EV_RESCORED 2     /* fp32 score fell inside rescore_margin; decision from the fp64 path */
+
+/* ewk_push flags */
+#define EWK_PUSH_DEVICE 1     /* pcm is a device pointer */
+
+typedef struct ewk_engine ewk_engine;
+
+/* Defaults mirror the reference constants (wakeword.py:31-48, 405-431, 1100-1118). */
+typedef struct ewk_config {
+    int32_t sample_rate;          /* 16000  SoundBuffer.FREQUENCY                  */
+    int32_t buffer_seconds;       /* 10     DEFAULT_BUFFER_SECONDS                 */
+    int32_t block;                /* 1600   samples per callback == per tick       */
+    int32_t reserved0;
+    double tick_seconds;          /* 0.1    time.sleep(0.1) in _detect_word        */
+    double pre_speech_silence;    /* 0.8    DEFAULT_PRE_SPEECH_SILENCE             */
+    double speech_duration_min;   /* 0.3    DEFAULT_SPEECH_DURATION_MIN            */
+    double speech_duration_max;   /* 2.0    DEFAULT_SPEECH_DURATION_MAX            */
+    double post_speech_silence;   /* 0.4    DEFAULT_POST_SPEECH_SILENCE            */
+    double padding;               /* 0.05   wakeword.py:1101                       */
+    double max_segment_seconds;   /* 3.0    wakeword.py:1115                       */
+    double similarity_threshold;  /* 75.0   WakeWord(similarity_threshold=)        */
+    double reentry_timeout;       /* <= 0: continuous; > 0: start()-mode re-entry every timeout s */
+    double min_threshold;         /* 0.005  SoundBuffer.MIN_THRESHOLD              */
+    double initial_threshold;     /* 0.01   SoundBuffer.silence_threshold init     */
+    double rescore_margin;        /* 1e-3   |score - threshold| re-scored in fp64  */
+} ewk_config;
+
+/* One level-1 pass (wakeword.py:1097-1124), with its level-2 result. */
+typedef struct ewk_event {
+    int32_t stream;
+    int32_t length;               /* len(word_audio)                               */
+    int64_t tick;                 /* virtual tick (time = tick * tick_seconds)     */
+    int64_t ring_start;           /* first sample of the segment inside the stream ring */
+    double time;
+    double score;                 /* scaled similarity (NaN allowed)               */
+    int32_t match;                /* score >= similarity_threshold                 */
+    int32_t flags;                /* EWK_EV_*                                      */
+} ewk_event;
+
+/* Per-stream gate state snapshot (SoundBuffer + _detect_word locals). */
+typedef struct ewk_stream_state {
+    int64_t samples_collected;
+    int64_t tick;
+    double silence_threshold;
+    double last_rms;
+    double silence_start_time;
+    double sound_start_time;
+    double sound_end_time;
+    double start_time;
+    int32_t pointer;
+    int32_t state;                /* 0 waiting, 1 in_silence, 2 in_sound, 3 after_sound */
+    int32_t started;              /* detection running (ring filled once)          */
+    int32_t last_silent;
+} ewk_stream_state;
+
+void ewk_default_config(ewk_config* cfg);
+const char* ewk_last_error(void);
+int ewk_abi_version(void);
+/* number of visible HIP devices (0 when none); never fails */
+int ewk_device_count(void);
+
+/* Engine: device index, number of concurrent streams (0 = scorer only). */
+int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config* cfg);
+void ewk_destroy(ewk_engine* e);
+int ewk_sync(ewk_engine* e);
+/* the engine's hipStream_t (as void*) */
+void* ewk_stream_handle(ewk_engine* e);
+
+/* ---- level 2: the matcher (WordMatcher, wakeword.py:520-639) ---------------- */
+
+/* WordMatcher.set_reference(audio) (wakeword.py:569-578): template = MFCC
+ * mean/std of `pcm` computed by the same HIP pipeline as every candidate. */
+int ewk_template_from_pcm(ewk_engine* e, const float* pcm, int64_t n);
+/* Direct template load (40 floats). */
+int ewk_set_template(ewk_engine* e, const float* mean20, const float* std20);
+/* Returns EWK_ENOTEMPLATE when none is set. */
+int ewk_get_template(ewk_engine* e, float* mean20, float* std20);
+/* WordMatcher.matches(audio, threshold) / WakeWord(similarity_threshold=) (wakeword.py:627-639, 676). */
+int ewk_set_similarity_threshold(ewk_engine* e, double threshold);
+
+/* WordMatcher.extract_mfcc + calculate_similarity + matches over a ragged
+ * batch (wakeword.py:544-639).  Segment i is pcm[offsets[i] : offsets[i] +
+ * lengths[i]].  Host buffers.  out_* may be NULL except out_score.  Without a
+ * template only mean/std are produced and out_score/out_match are left alone
+ * (no error) when `require_template` is 0. */
+int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm,
+                       const int64_t* offsets, const int32_t* lengths, int32_t n_seg,
+                       float* out_mean, float* out_std, double* out_score, uint8_t* out_match,
+                       int32_t require_template);
+
+/* Device-resident variant: every pointer is device memory; `stream` is a
+ * hipStream_t (NULL = the engine stream).  Asynchronous; no host sync. */
+int ewk_score_segments_device(ewk_engine* e, const float* d_pcm,
+                              const int64_t* d_offsets, const int32_t* d_lengths, int32_t n_seg,
+                              float* d_mean, float* d_std, double* d_score, uint8_t* d_match,
+                              void* stream);
+
+/* fp64 reference-precision scorer (the rescoring path) on host buffers. */
+int ewk_score_segments_f64(ewk_engine* e, const float* pcm, int64_t n_pcm,
+                           const int64_t* offsets, const int32_t* lengths, int32_t n_seg,
+                           double* out_mean, double* out_std, double* out_score);
+
+/* ---- level 1 + 2: the streaming gate (SoundBuffer + _detect_word) ------------ */
+
+/* One tick for every stream: SoundBuffer._add_sound_to_buffer with a `block`
+ * sample callback per stream (wakeword.py:454-486), then is_silent()
+ * (wakeword.py:488-513) and one _detect_word FSM step (wakeword.py:1059-1118).
+ * Stream s's samples are pcm[s*stride : s*stride + block].  Segments that pass
+ * level 1 are scored on the device (level 2) and queued as events. */
+int ewk_push(ewk_engine* e, const float* pcm, int64_t stride, int32_t flags);
+/* Same for n_ticks consecutive ticks: tick t of stream s is
+ * pcm[s*stride + t*tick_stride ...]. One launch sequence, no host sync. */
+int ewk_push_many(ewk_engine* e, const float* pcm, int64_t stride, int64_t tick_stride,
+                  int32_t n_ticks, int32_t flags);
+/* Drain up to `cap` queued events (blocks on the engine stream). */
+int ewk_poll(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out);
+int ewk_get_stream_state(ewk_engine* e, int32_t stream, ewk_stream_state* out);
+/* SoundBuffer.return_last_n_seconds(n) (wakeword.py:498-513) as float32 (ring values are the float32 input). */
+int ewk_read_last(ewk_engine* e, int32_t stream, int64_t n_samples, float* out, int64_t* n_out);
+/* Copy the samples of a queued/polled event (ring must not have wrapped over it). */
+int ewk_read_segment(ewk_engine* e, int32_t stream, int64_t ring_start, int32_t length, float* out);
+/* Reset all stream state (ring, threshold, FSM, event queue). */
+int ewk_reset_streams(ewk_engine* e);
+
+/* ---- measurement ------------------------------------------------------------ */
+/* When enabled, every scorer / gate launch is bracketed by hipEvents on the
+ * stream it runs on; ewk_profile_read resolves them (synchronizing) and returns
+ * the summed device time and launch count per kernel family, then clears.
+ * kind: 0 = fp32 MFCC scorer (k_score_f32), 1 = fp64 re-scorer, 2 = gate ticks. */
+int ewk_profile_enable(ewk_engine* e, int32_t on);
+int ewk_profile_read(ewk_engine* e, int32_t kind, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EWK_H */

@@ -1,0 +1,130 @@
+"""Level-1 (+2) parity on the GPU: the streaming engine vs traces of the REAL
+reference SoundBuffer + WakeWord._detect_word (tests/golden/gate_traces.json)
+and vs the oracle restatement (oracle/gate_ref.py) on many streams.
+
+Bar: bit-identical gate decisions (per-tick is_silent, thresholds, segment
+ticks/lengths/samples), scores within 1e-4, identical match decisions.
+"""
+import numpy as np
+import pytest
+
+import synth
+from golden_io import gate_fixture, matcher_fixture, score_close, sha, stream_pcm, template_arrays
+from oracle import mfcc_ref
+from oracle.gate_ref import GateConfig, run_stream
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(n, gate, **extra):
+    from easywakeword_amd import StreamEngine
+    kw = dict(pre_speech_silence=gate["pre_speech_silence"], speech_duration_min=gate["speech_duration_min"],
+              speech_duration_max=gate["speech_duration_max"], post_speech_silence=gate["post_speech_silence"],
+              buffer_seconds=gate.get("buffer_seconds", 10), block=gate.get("block", 1600),
+              reentry_timeout=float(gate.get("reentry_timeout") or 0.0))
+    kw.update(extra)
+    return StreamEngine(n, **kw)
+
+
+@pytest.fixture(scope="module")
+def template():
+    fx, _ = matcher_fixture()
+    return template_arrays(fx)
+
+
+@pytest.mark.parametrize("rec", gate_fixture(), ids=lambda r: r["name"])
+def test_reference_trace_tick_by_tick(rec, template):
+    pcm = stream_pcm(rec)
+    eng = _engine(1, rec["gate"])
+    eng.set_template(*template)
+    block = rec["gate"]["block"]
+    silent = {}
+    thr = {}
+    for (k, s), t in zip(rec["silent"], rec["threshold"]):
+        silent.setdefault(k, []).append(s)
+        thr.setdefault(k, []).append(t)
+    events = []
+    for k in range(len(pcm) // block):
+        eng.push(pcm[k * block:(k + 1) * block].reshape(1, -1))
+        st = eng.state(0)
+        tick = k + 1
+        if tick in silent:   # every is_silent() the reference made at this clock value
+            assert all(bool(st["last_silent"]) == s for s in silent[tick]), (tick, st, silent[tick])
+            assert all(st["silence_threshold"] == t for t in thr[tick]), (tick, st["silence_threshold"], thr[tick])
+        for ev in eng.poll():
+            if ev["flags"] & 1:
+                continue
+            audio = eng.read_segment(0, int(ev["ring_start"]), int(ev["length"]))
+            events.append((int(ev["tick"]), int(ev["length"]), sha(audio.astype(np.float64)), float(ev["score"]),
+                           bool(ev["match"])))
+    ref = [(e["tick"], e["length"], e["sha256"], e["score"], e["match"]) for e in rec["events"]]
+    assert [e[:3] for e in events] == [r[:3] for r in ref]
+    for e, r in zip(events, ref):
+        assert score_close(e[3], r[3], 1e-4), (e, r)
+        assert e[4] == r[4]
+
+
+def _oracle_events(pcm, gate):
+    cfg = GateConfig(pre_speech_silence=gate["pre_speech_silence"], speech_duration_min=gate["speech_duration_min"],
+                     speech_duration_max=gate["speech_duration_max"],
+                     post_speech_silence=gate["post_speech_silence"], block=gate.get("block", 1600),
+                     reentry_timeout=gate.get("reentry_timeout"))
+    return run_stream(pcm, cfg).events
+
+
+def test_many_streams_vs_oracle(template):
+    """32 streams with different gains / noise / distractors, pushed 16 ticks at a time."""
+    gate = dict(pre_speech_silence=0.8, speech_duration_min=0.3, speech_duration_max=2.0, post_speech_silence=0.4)
+    n = 32
+    pcms = []
+    for i in range(n):
+        rng = np.random.default_rng(500 + i)
+        p, _ = synth.make_stream(seed=2000 + i, n_words=4, sigma=float(rng.uniform(1e-4, 5e-3)),
+                                 gain=float(rng.uniform(0.2, 3.0)), distractors=bool(i % 2))
+        pcms.append(p)
+    L = min(len(p) for p in pcms)
+    L -= L % 1600
+    data = np.stack([p[:L] for p in pcms]).astype(np.float32)
+    eng = _engine(n, gate)
+    eng.set_template(*template)
+    got = []
+    step = 16 * 1600
+    for c in range(0, L, step):
+        eng.push_many(data[:, c:c + step])
+        got.extend(eng.poll().tolist())
+    tm, ts = template
+    n_ev = 0
+    for i in range(n):
+        ref = _oracle_events(data[i], gate)
+        mine = sorted([g for g in got if g[0] == i], key=lambda g: g[2])
+        assert [(g[2], g[1], bool(g[7] & 1)) for g in mine] == [(e.tick, e.length, e.skipped) for e in ref], i
+        for g, e in zip(mine, ref):
+            if e.skipped:
+                continue
+            cm, cs = mfcc_ref.extract_mfcc(e.audio)
+            s = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
+            assert score_close(g[5], s, 1e-4), (i, g, s)
+            assert bool(g[6]) == (s >= 75.0)
+            n_ev += 1
+    assert n_ev > 20
+
+
+def test_unaligned_block_512_thresholds():
+    """frame_size 512: 312 physical blocks, the write pointer is not block-aligned
+    after the first wrap -> exercises the incremental block-RMS refresh."""
+    gate = dict(pre_speech_silence=0.8, speech_duration_min=0.3, speech_duration_max=2.0,
+                post_speech_silence=0.4, block=512)
+    pcm, _ = synth.make_stream(seed=77, n_words=3, sigma=2e-3, gain=1.0, block=512)
+    eng = _engine(1, gate)
+    cfg = GateConfig(block=512)
+    from oracle.gate_ref import DetectorRef
+    det = DetectorRef(cfg)
+    for k in range(len(pcm) // 512):
+        blk = pcm[k * 512:(k + 1) * 512]
+        eng.push(blk.reshape(1, -1))
+        det.push_tick(blk)
+        st = eng.state(0)
+        assert st["silence_threshold"] == det.buf.silence_threshold, k
+        if det.started and det.buf.is_buffer_full():
+            assert bool(st["last_silent"]) == det.buf.is_silent(), k
+            assert st["state"] == det.state, k
