@@ -25,6 +25,8 @@ EWK_ENODEV = -5
 EWK_EV_SKIPPED = 1
 EWK_EV_RESCORED = 2
 EWK_PUSH_DEVICE = 1
+EWK_SCORE_REQUIRE_TEMPLATE = 1
+EWK_SCORE_F32_CANDIDATES = 2
 
 # Every symbol include/ewk.h declares (checked by tests/test_capi.py).
 EXPORTS = [
@@ -106,8 +108,9 @@ def load():
             "ewk_set_similarity_threshold": (C.c_int, [_P, C.c_double]),
             "ewk_score_segments": (C.c_int, [_P, _fp, C.c_int64, _i64p, _i32p, C.c_int32, _fp, _fp, _dp, _u8p,
                                              C.c_int32]),
-            "ewk_score_segments_device": (C.c_int, [_P, _P, _P, _P, C.c_int32, _P, _P, _P, _P, _P]),
-            "ewk_score_segments_f64": (C.c_int, [_P, _fp, C.c_int64, _i64p, _i32p, C.c_int32, _dp, _dp, _dp]),
+            "ewk_score_segments_device": (C.c_int, [_P, _P, _P, _P, C.c_int32, _P, _P, _P, _P, C.c_int32, _P]),
+            "ewk_score_segments_f64": (C.c_int, [_P, _fp, C.c_int64, _i64p, _i32p, C.c_int32, _dp, _dp, _dp,
+                                                 C.c_int32]),
             "ewk_push": (C.c_int, [_P, _P, C.c_int64, C.c_int32]),
             "ewk_push_many": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.c_int32, C.c_int32]),
             "ewk_poll": (C.c_int, [_P, C.POINTER(EwkEvent), C.c_int32, _i32p]),

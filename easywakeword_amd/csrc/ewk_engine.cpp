@@ -332,8 +332,10 @@ static ScoreArgs base_args(ewk_engine* e) {
 
 // f32 scorer + fp64 rescoring of the near-threshold list, all on `s`.
 static int score_linear(ewk_engine* e, const float* d_pcm, const int64_t* d_off, const int32_t* d_len, int32_t n,
-                        float* d_mean, float* d_std, double* d_score, uint8_t* d_match, hipStream_t s) {
+                        float* d_mean, float* d_std, double* d_score, uint8_t* d_match, int32_t flags,
+                        hipStream_t s) {
     ScoreArgs a = base_args(e);
+    a.cand_f32 = (flags & EWK_SCORE_F32_CANDIDATES) ? 1 : 0;
     a.pcm = d_pcm;
     a.offsets = d_off;
     a.lengths = d_len;
@@ -358,15 +360,17 @@ static int score_linear(ewk_engine* e, const float* d_pcm, const int64_t* d_off,
 
 int ewk_score_segments_device(ewk_engine* e, const float* d_pcm, const int64_t* d_offsets, const int32_t* d_lengths,
                               int32_t n_seg, float* d_mean, float* d_std, double* d_score, uint8_t* d_match,
-                              void* stream) {
+                              int32_t flags, void* stream) {
     if (!e) return fail(EWK_EINVAL, "engine is NULL");
     if (n_seg < 0) return fail(EWK_EINVAL, "n_seg must be >= 0");
     if (n_seg == 0) return EWK_OK;
     if (!d_pcm || !d_offsets || !d_lengths) return fail(EWK_EINVAL, "NULL device pointer");
+    if ((flags & EWK_SCORE_REQUIRE_TEMPLATE) && !e->has_tmpl)
+        return fail(EWK_ENOTEMPLATE, "No reference word set. Call set_reference() first.");
     if (e->has_tmpl && !d_score) return fail(EWK_EINVAL, "d_score is required when a template is set");
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-    return score_linear(e, d_pcm, d_offsets, d_lengths, n_seg, d_mean, d_std, d_score, d_match, s);
+    return score_linear(e, d_pcm, d_offsets, d_lengths, n_seg, d_mean, d_std, d_score, d_match, flags, s);
 }
 
 static int check_segments(const int64_t* offsets, const int32_t* lengths, int32_t n_seg, int64_t n_pcm,
@@ -383,10 +387,10 @@ static int check_segments(const int64_t* offsets, const int32_t* lengths, int32_
 
 int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int64_t* offsets,
                        const int32_t* lengths, int32_t n_seg, float* out_mean, float* out_std, double* out_score,
-                       uint8_t* out_match, int32_t require_template) {
+                       uint8_t* out_match, int32_t flags) {
     if (!e) return fail(EWK_EINVAL, "engine is NULL");
     if (n_seg < 0 || n_pcm < 0) return fail(EWK_EINVAL, "negative size");
-    if (require_template && !e->has_tmpl)
+    if ((flags & EWK_SCORE_REQUIRE_TEMPLATE) && !e->has_tmpl)
         return fail(EWK_ENOTEMPLATE, "No reference word set. Call set_reference() first.");
     if (n_seg == 0) return EWK_OK;
     if (!offsets || !lengths || (n_pcm > 0 && !pcm)) return fail(EWK_EINVAL, "NULL argument");
@@ -422,6 +426,7 @@ int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int
         a.out_std = e->stdv.p;
         a.out_score = e->score.p;
         a.out_match = e->match.p;
+        a.cand_f32 = (flags & EWK_SCORE_F32_CANDIDATES) ? 1 : 0;
         if (!a.has_template) a.rescore_list = nullptr;
         HIP_TRY(hipMemsetAsync(e->d_rescore, 0, sizeof(int32_t), s));
         HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));
@@ -443,7 +448,7 @@ int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int
 
 int ewk_score_segments_f64(ewk_engine* e, const float* pcm, int64_t n_pcm, const int64_t* offsets,
                            const int32_t* lengths, int32_t n_seg, double* out_mean, double* out_std,
-                           double* out_score) {
+                           double* out_score, int32_t flags) {
     if (!e) return fail(EWK_EINVAL, "engine is NULL");
     if (n_seg < 0 || n_pcm < 0) return fail(EWK_EINVAL, "negative size");
     if (n_seg == 0) return EWK_OK;
@@ -472,6 +477,7 @@ int ewk_score_segments_f64(ewk_engine* e, const float* pcm, int64_t n_pcm, const
     a.lengths = e->lengths.p;
     a.n_seg = n_seg;
     a.out_score = e->score.p;
+    a.cand_f32 = (flags & EWK_SCORE_F32_CANDIDATES) ? 1 : 0;
     a.rescore_list = nullptr;
     a.rescore_count = nullptr;
     HIP_TRY(launch_score_f64(e->d_tab64, a, 0, e->f64_scratch.p, per, e->f64_grid, e->mean64.p, e->std64.p, s));
@@ -491,7 +497,7 @@ int ewk_template_from_pcm(ewk_engine* e, const float* pcm, int64_t n) {
     float m[NMFCC], sd[NMFCC];
     const bool had = e->has_tmpl;
     e->has_tmpl = false;   // compute stats only
-    int rc = ewk_score_segments(e, pcm, n, &off, &len, 1, m, sd, nullptr, nullptr, 0);
+    int rc = ewk_score_segments(e, pcm, n, &off, &len, 1, m, sd, nullptr, nullptr, EWK_SCORE_F32_CANDIDATES);
     e->has_tmpl = had;
     if (rc) return rc;
     return ewk_set_template(e, m, sd);

@@ -62,6 +62,7 @@ struct ScoreArgs {
     int64_t ring_len;
     int32_t n_seg;            // linear mode count, ring mode capacity
     int32_t has_template;
+    int32_t cand_f32;         // candidate dtype of the reference path: 1 float32, 0 float64
     const float* tmpl;        // [40] template mean[20], std[20]
     float* out_mean;
     float* out_std;

@@ -283,26 +283,78 @@ __device__ void segment_stats(const SegView& v, const unsigned char* smem, float
     }
 }
 
-__device__ __forceinline__ double wave_sum(double x) {
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) x += __shfl_xor(x, m, 64);
-    return x;
+// ---- the score, exactly as WordMatcher.calculate_similarity evaluates it --------
+// (wakeword.py:611-625 with scipy 1.15 `correlation`: dist = clip(1 - uv/sqrt(uu*vv), 0, 2)).
+// The template u is float32 (librosa.load -> float32 MFCCs).  numpy's dot of two
+// float32 vectors is float(sum_double(float(a*b))) (cblas_sdot's scalar path for
+// n = 20, verified bit for bit against np.dot); a float32 x float64 or float64 dot
+// is a float64 dot.  Two candidate dtypes occur in the reference:
+//   float64 (streaming: SoundBuffer slices, wakeword.py:428, 509-513): uu is a
+//     float32 dot, uv / vv float64, the rest float64;
+//   float32 (WordMatcher on float32 audio): every dot float32 and, under NumPy 2
+//     scalar promotion, every following operation float32.
+__device__ __forceinline__ float sdot20(const float* a, const float* b) {
+#pragma clang fp contract(off)
+    double acc = 0.0;
+    for (int i = 0; i < NMFCC; ++i) acc += (double)(a[i] * b[i]);
+    return (float)acc;
 }
 
-// scipy 1.15 correlation/cosine: dist = clip(1 - uv/sqrt(uu*vv), 0, 2), NaN kept.
-__device__ __forceinline__ double cosine_dist(double uv, double uu, double vv) {
+template <typename T>
+__device__ __forceinline__ double ddot20(const float* a, const T* b) {
 #pragma clang fp contract(off)
-    double d = 1.0 - uv / sqrt(uu * vv);
-    if (d < 0.0) d = 0.0;
-    else if (d > 2.0) d = 2.0;
+    double acc = 0.0;
+    for (int i = 0; i < NMFCC; ++i) acc += (double)a[i] * (double)b[i];
+    return acc;
+}
+
+template <typename T>
+__device__ __forceinline__ double ddot20s(const T* a) {
+#pragma clang fp contract(off)
+    double acc = 0.0;
+    for (int i = 0; i < NMFCC; ++i) acc += (double)a[i] * (double)a[i];
+    return acc;
+}
+
+__device__ __forceinline__ double clip02(double d) {
+    if (d < 0.0) return 0.0;
+    if (d > 2.0) return 2.0;
+    return d;   // NaN passes through (np.clip)
+}
+
+__device__ __forceinline__ float clip02f(float d) {
+    if (d < 0.0f) return 0.0f;
+    if (d > 2.0f) return 2.0f;
     return d;
 }
 
-__device__ __forceinline__ double scaled_similarity(double sm, double ss) {
+// Candidate stats in float64 (the streaming dtype).
+__device__ double score_f64cand(const float* tm, const float* ts, const double* cm, const double* cs) {
 #pragma clang fp contract(off)
+    const double uu_m = (double)sdot20(tm, tm), uu_s = (double)sdot20(ts, ts);
+    const double sm = 1.0 - clip02(1.0 - ddot20(tm, cm) / sqrt(uu_m * ddot20s(cm)));
+    const double ss = 1.0 - clip02(1.0 - ddot20(ts, cs) / sqrt(uu_s * ddot20s(cs)));
     const double combined = sm * 0.7 + ss * 0.3;
     const double percent = combined * 100.0;
-    return pow(percent, 1.5) / 10.0;   // 100**0.5 == 10.0 exactly
+    return pow(percent, 1.5) / 10.0;   // (100**0.5) == 10.0 exactly
+}
+
+// Candidate stats in float32 (WordMatcher on float32 audio): float32 arithmetic.
+__device__ double score_f32cand(const float* tm, const float* ts, const float* cm, const float* cs) {
+#pragma clang fp contract(off)
+    float sim[2];
+    for (int k = 0; k < 2; ++k) {
+        const float* u = k ? ts : tm;
+        const float* v = k ? cs : cm;
+        const float uu = sdot20(u, u), vv = sdot20(v, v), uv = sdot20(u, v);
+        const float prod = uu * vv;                       // float32 * float32
+        const float root = (float)sqrt((double)prod);      // math.sqrt, back to float32 (NEP 50)
+        const float dist = clip02f(1.0f - uv / root);
+        sim[k] = 1.0f - dist;
+    }
+    const float combined = sim[0] * 0.7f + sim[1] * 0.3f;
+    const float percent = combined * 100.0f;
+    return (double)(powf(percent, 1.5f) / 10.0f);
 }
 
 template <int RING>
@@ -386,17 +438,12 @@ __global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__
         }
     }
     if (!a.has_template) continue;
-    double tm = 0.0, ts = 0.0;
-    if (lane < NMFCC) {
-        tm = a.tmpl[lane];
-        ts = a.tmpl[NMFCC + lane];
-    }
-    const double uv_m = wave_sum(tm * (double)cm), uu_m = wave_sum(tm * tm), vv_m = wave_sum((double)cm * cm);
-    const double uv_s = wave_sum(ts * (double)cs), uu_s = wave_sum(ts * ts), vv_s = wave_sum((double)cs * cs);
     if (lane == 0) {
-        const double sm = 1.0 - cosine_dist(uv_m, uu_m, vv_m);
-        const double ss = 1.0 - cosine_dist(uv_s, uu_s, vv_s);
-        const double score = scaled_similarity(sm, ss);
+        float c32[2 * NMFCC];
+        double c64[2 * NMFCC];
+        for (int i = 0; i < 2 * NMFCC; ++i) { c32[i] = misc[i]; c64[i] = (double)misc[i]; }
+        const double score = a.cand_f32 ? score_f32cand(a.tmpl, a.tmpl + NMFCC, c32, c32 + NMFCC)
+                                        : score_f64cand(a.tmpl, a.tmpl + NMFCC, c64, c64 + NMFCC);
         const int match = score >= a.threshold;
         const bool near = fabs(score - a.threshold) < a.rescore_margin;
         if (RING) {
@@ -555,14 +602,14 @@ __global__ __launch_bounds__(256) void k_score_f64(const Tables64* __restrict__ 
         }
         __syncthreads();
         if (tid == 0 && a.has_template) {
-            double uvm = 0, uum = 0, vvm = 0, uvs = 0, uus = 0, vvs = 0;
-            for (int k = 0; k < NMFCC; ++k) {
-                const double tm = a.tmpl[k], ts = a.tmpl[NMFCC + k];
-                const double cm = s_stat[k], cs = s_stat[NMFCC + k];
-                uvm += tm * cm; uum += tm * tm; vvm += cm * cm;
-                uvs += ts * cs; uus += ts * ts; vvs += cs * cs;
+            double score;
+            if (a.cand_f32) {
+                float c32[2 * NMFCC];
+                for (int i = 0; i < 2 * NMFCC; ++i) c32[i] = (float)s_stat[i];
+                score = score_f32cand(a.tmpl, a.tmpl + NMFCC, c32, c32 + NMFCC);
+            } else {
+                score = score_f64cand(a.tmpl, a.tmpl + NMFCC, s_stat, s_stat + NMFCC);
             }
-            const double score = scaled_similarity(1.0 - cosine_dist(uvm, uum, vvm), 1.0 - cosine_dist(uvs, uus, vvs));
             const int match = score >= a.threshold;
             if (RING) {
                 a.events[seg].score = score;

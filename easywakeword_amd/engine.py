@@ -97,9 +97,17 @@ class Engine:
         self.config.similarity_threshold = float(threshold)
 
     # -- level 2 over ragged host batches ------------------------------------
-    def score(self, segments, require_template: bool = True):
+    def score(self, segments, require_template: bool = True, candidate_dtype: str = "auto"):
         """MFCC stats + score of a list of 1-D arrays.  Returns
-        (mean[n,20] f32, std[n,20] f32, score[n] f64, match[n] bool)."""
+        (mean[n,20] f32, std[n,20] f32, score[n] f64, match[n] bool).
+
+        candidate_dtype selects the reference arithmetic of the score:
+        "float64" (SoundBuffer slices, the streaming path), "float32"
+        (WordMatcher fed float32 audio) or "auto" (float32 iff every segment is)."""
+        if candidate_dtype == "auto":
+            f32 = all(np.asarray(s).dtype == np.float32 for s in segments) and len(segments) > 0
+        else:
+            f32 = np.dtype(candidate_dtype) == np.float32
         segs = [_f32(s) for s in segments]
         n = len(segs)
         lengths = np.array([len(s) for s in segs], dtype=np.int32)
@@ -108,10 +116,10 @@ class Engine:
             offsets[1:] = np.cumsum(lengths[:-1], dtype=np.int64)
         pcm = np.concatenate(segs) if n else np.zeros(0, np.float32)
         pcm = np.ascontiguousarray(pcm, dtype=np.float32)
-        return self.score_packed(pcm, offsets, lengths, require_template)
+        return self.score_packed(pcm, offsets, lengths, require_template, f32)
 
     def score_packed(self, pcm: np.ndarray, offsets: np.ndarray, lengths: np.ndarray,
-                     require_template: bool = True):
+                     require_template: bool = True, f32_candidates: bool = False):
         pcm = np.ascontiguousarray(pcm, dtype=np.float32)
         offsets = np.ascontiguousarray(offsets, dtype=np.int64)
         lengths = np.ascontiguousarray(lengths, dtype=np.int32)
@@ -122,11 +130,18 @@ class Engine:
         match = np.zeros(n, np.uint8)
         check(self._lib.ewk_score_segments(self._h, _lib.fptr(pcm), len(pcm), _lib.i64ptr(offsets),
                                            _lib.i32ptr(lengths), n, _lib.fptr(mean), _lib.fptr(std),
-                                           _lib.dptr(score), _lib.u8ptr(match), int(bool(require_template))))
+                                           _lib.dptr(score), _lib.u8ptr(match), self._flags(require_template,
+                                                                                            f32_candidates)))
         return mean, std, score, match.astype(bool)
 
-    def score_f64(self, segments):
+    @staticmethod
+    def _flags(require_template: bool, f32: bool) -> int:
+        return (_lib.EWK_SCORE_REQUIRE_TEMPLATE if require_template else 0) | \
+            (_lib.EWK_SCORE_F32_CANDIDATES if f32 else 0)
+
+    def score_f64(self, segments, candidate_dtype: str = "float64"):
         """Reference-precision (float64) path: (mean[n,20], std[n,20], score[n])."""
+        f32 = np.dtype(candidate_dtype) == np.float32
         segs = [_f32(s) for s in segments]
         n = len(segs)
         lengths = np.array([len(s) for s in segs], dtype=np.int32)
@@ -139,16 +154,18 @@ class Engine:
         score = np.full(n, np.nan, np.float64)
         check(self._lib.ewk_score_segments_f64(self._h, _lib.fptr(pcm), len(pcm), _lib.i64ptr(offsets),
                                                _lib.i32ptr(lengths), n, _lib.dptr(mean), _lib.dptr(std),
-                                               _lib.dptr(score)))
+                                               _lib.dptr(score), self._flags(False, f32)))
         return mean, std, score
 
     def score_device(self, pcm_ptr: int, offsets_ptr: int, lengths_ptr: int, n: int, mean_ptr: int,
-                     std_ptr: int, score_ptr: int, match_ptr: int, stream: int = 0) -> None:
+                     std_ptr: int, score_ptr: int, match_ptr: int, stream: int = 0,
+                     f32_candidates: bool = False) -> None:
         """Device-resident batch (e.g. torch tensor data_ptr()s); asynchronous on `stream`."""
         check(self._lib.ewk_score_segments_device(self._h, C.c_void_p(pcm_ptr), C.c_void_p(offsets_ptr),
                                                   C.c_void_p(lengths_ptr), int(n), C.c_void_p(mean_ptr or None),
                                                   C.c_void_p(std_ptr or None), C.c_void_p(score_ptr or None),
-                                                  C.c_void_p(match_ptr or None), C.c_void_p(stream or None)))
+                                                  C.c_void_p(match_ptr or None), self._flags(False, f32_candidates),
+                                                  C.c_void_p(stream or None)))
 
 
 class StreamEngine(Engine):

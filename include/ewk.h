@@ -42,6 +42,12 @@ extern "C" {
 #define EWK_EV_SKIPPED 1      /* segment longer than max_segment_seconds: no level-2 call (wakeword.py:1113-1118) */
 #define EWK_EV_RESCORED 2     /* fp32 score fell inside rescore_margin; decision from the fp64 path */
 
+/* ewk_score_segments* flags */
+#define EWK_SCORE_REQUIRE_TEMPLATE 1   /* EWK_ENOTEMPLATE when no template (calculate_similarity) */
+#define EWK_SCORE_F32_CANDIDATES 2     /* score with the reference's float32-candidate arithmetic
+                                          (WordMatcher fed float32 audio); default: float64
+                                          candidates, as SoundBuffer slices are (wakeword.py:428) */
+
 /* ewk_push flags */
 #define EWK_PUSH_DEVICE 1     /* pcm is a device pointer */
 
@@ -122,25 +128,24 @@ int ewk_set_similarity_threshold(ewk_engine* e, double threshold);
 
 /* WordMatcher.extract_mfcc + calculate_similarity + matches over a ragged
  * batch (wakeword.py:544-639).  Segment i is pcm[offsets[i] : offsets[i] +
- * lengths[i]].  Host buffers.  out_* may be NULL except out_score.  Without a
- * template only mean/std are produced and out_score/out_match are left alone
- * (no error) when `require_template` is 0. */
+ * lengths[i]].  Host buffers; any out_* may be NULL.  Without a template only
+ * mean/std are produced (EWK_ENOTEMPLATE if flags has EWK_SCORE_REQUIRE_TEMPLATE). */
 int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm,
                        const int64_t* offsets, const int32_t* lengths, int32_t n_seg,
                        float* out_mean, float* out_std, double* out_score, uint8_t* out_match,
-                       int32_t require_template);
+                       int32_t flags);
 
 /* Device-resident variant: every pointer is device memory; `stream` is a
  * hipStream_t (NULL = the engine stream).  Asynchronous; no host sync. */
 int ewk_score_segments_device(ewk_engine* e, const float* d_pcm,
                               const int64_t* d_offsets, const int32_t* d_lengths, int32_t n_seg,
                               float* d_mean, float* d_std, double* d_score, uint8_t* d_match,
-                              void* stream);
+                              int32_t flags, void* stream);
 
 /* fp64 reference-precision scorer (the rescoring path) on host buffers. */
 int ewk_score_segments_f64(ewk_engine* e, const float* pcm, int64_t n_pcm,
                            const int64_t* offsets, const int32_t* lengths, int32_t n_seg,
-                           double* out_mean, double* out_std, double* out_score);
+                           double* out_mean, double* out_std, double* out_score, int32_t flags);
 
 /* ---- level 1 + 2: the streaming gate (SoundBuffer + _detect_word) ------------ */
 

@@ -1,0 +1,26 @@
+#!/bin/bash
+# One GPU session: tests, smoke, bench, rocprof.  Stops at the first GPU fault/timeout.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+MODE=${1:-all}
+ok_or_testfail() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
+if [ "$MODE" = all ] || [ "$MODE" = test ]; then
+  timeout -k 10 900 python -m pytest tests -q -m gpu -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
+  ok_or_testfail $rc || exit $rc
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+  rc=$?; echo "smoke rc=$rc"; tail -5 gpurun_out/smoke.log
+  ok_or_testfail $rc || exit $rc
+fi
+if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
+  timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.log 2>&1
+  rc=$?; echo "bench rc=$rc"; tail -c 3000 gpurun_out/bench.log
+  [ $rc -eq 0 ] || exit $rc
+fi
+if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
+  cd /tmp && export TMPDIR=/tmp
+  R="${GRAFT_REPO_ROOT:-/root/repo}"
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "$R/gpurun_out/prof.log" 2>&1
+  rc=$?; echo "rocprof rc=$rc"; tail -5 "$R/gpurun_out/prof.log"
+  find "$R/gpurun_out/prof" -name "*stats*" | head
+fi

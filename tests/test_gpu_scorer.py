@@ -46,7 +46,7 @@ def test_golden_scores_and_decisions(engine, fixture, ref_dtype):
     engine.set_template(*template_arrays(fx))
     engine.set_threshold(75.0)
     names = [c["name"] for c in fx["cases"]]
-    mean, std, score, match = engine.score([audio[n] for n in names])
+    mean, std, score, match = engine.score([audio[n] for n in names], candidate_dtype=ref_dtype)
     bad = []
     for i, c in enumerate(fx["cases"]):
         ref = c[ref_dtype]
@@ -79,7 +79,7 @@ def test_random_ragged_batch_vs_oracle(engine):
     engine.template_from_pcm(word)
     tm, ts = engine.get_template()
     segs = synth.ragged_segments(4321, 200, 160, 48000)
-    _, _, score, match = engine.score(segs)
+    _, _, score, match = engine.score(segs, candidate_dtype="float64")
     worst = 0.0
     for i, x in enumerate(segs):
         cm, cs = mfcc_ref.extract_mfcc(x.astype(np.float64))
@@ -133,10 +133,10 @@ def test_near_threshold_decisions_are_exact(engine):
         if math.isnan(s64[i]):
             continue
         engine.set_threshold(float(s64[i]))
-        _, _, sc, mt = engine.score([x])
+        _, _, sc, mt = engine.score([x], candidate_dtype="float64")
         assert bool(mt[0]), (i, sc[0], s64[i])
         engine.set_threshold(float(np.nextafter(s64[i], np.inf)))
-        _, _, sc, mt = engine.score([x])
+        _, _, sc, mt = engine.score([x], candidate_dtype="float64")
         assert not bool(mt[0]), (i, sc[0], s64[i])
     engine.set_threshold(75.0)
 
@@ -146,7 +146,7 @@ def test_edge_lengths(engine):
     tm, ts = engine.get_template()
     segs = [np.full(n, 0.1, np.float32) * np.sin(np.arange(n, dtype=np.float32)) for n in
             (1, 2, 159, 160, 161, 255, 256, 257, 511, 512, 513, 2559, 2560, 2561, 48000, 48161)]
-    _, _, score, _ = engine.score(segs)
+    _, _, score, _ = engine.score(segs, candidate_dtype="float64")
     for i, x in enumerate(segs):
         cm, cs = mfcc_ref.extract_mfcc(x.astype(np.float64))
         ref = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
