@@ -69,7 +69,8 @@ struct ewk_engine {
     bool has_tmpl = false;
 
     // rescoring
-    int32_t* d_rescore = nullptr;   // [0] = count, [1..] list
+    DevBuf<int32_t> rescore_buf;    // [0] = count, [1..] list
+    int32_t* d_rescore = nullptr;   // == rescore_buf.p
     int32_t* d_work = nullptr;      // scorer work counter
     int32_t rescore_cap = 4096;
     DevBuf<double> f64_scratch;
@@ -92,6 +93,9 @@ struct ewk_engine {
     int32_t* d_evc = nullptr;   // [0] count, [1] dropped, [2] scored watermark
     int32_t ev_cap = 0;
     DevBuf<float> push_stage;
+    float* h_stage = nullptr;       // pinned host staging for ewk_push / ewk_push_many
+    size_t h_stage_cap = 0;
+    hipEvent_t h_stage_free = nullptr;   // recorded after the last DMA out of h_stage
     int64_t tick = 0;
     int32_t lds_gate = 0;
 
@@ -135,6 +139,18 @@ static void zero_event_state(ewk_engine* e) {
     if (e->d_evc) (void)hipMemsetAsync(e->d_evc, 0, 4 * sizeof(int32_t), e->stream);
 }
 
+// The re-score list holds at most one entry per segment of a launch.
+static hipError_t reserve_rescore(ewk_engine* e, int32_t n_seg) {
+    if (n_seg <= e->rescore_cap) return hipSuccess;
+    hipError_t err = hipStreamSynchronize(e->stream);
+    if (err != hipSuccess) return err;
+    err = e->rescore_buf.reserve((size_t)n_seg + 1);
+    if (err != hipSuccess) return err;
+    e->d_rescore = e->rescore_buf.p;
+    e->rescore_cap = n_seg;
+    return hipSuccess;
+}
+
 extern "C" {
 
 void ewk_default_config(ewk_config* c) {
@@ -172,7 +188,7 @@ void ewk_destroy(ewk_engine* e) {
     (void)hipFree(e->d_tab);
     (void)hipFree(e->d_tab64);
     (void)hipFree(e->d_tmpl);
-    (void)hipFree(e->d_rescore);
+    e->rescore_buf.release();
     (void)hipFree(e->d_work);
     e->f64_scratch.release();
     e->pcm.release();
@@ -190,6 +206,8 @@ void ewk_destroy(ewk_engine* e) {
     (void)hipFree(e->d_st);
     (void)hipFree(e->d_events);
     (void)hipFree(e->d_evc);
+    if (e->h_stage) (void)hipHostFree(e->h_stage);
+    if (e->h_stage_free) (void)hipEventDestroy(e->h_stage_free);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }
@@ -250,8 +268,8 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
             return bail(err, "tables64");
     }
     if ((err = hipMalloc(&e->d_tmpl, 2 * NMFCC * sizeof(float))) != hipSuccess) return bail(err, "template");
-    if ((err = hipMalloc(&e->d_rescore, (1 + e->rescore_cap) * sizeof(int32_t))) != hipSuccess)
-        return bail(err, "rescore");
+    if ((err = e->rescore_buf.reserve(1 + e->rescore_cap)) != hipSuccess) return bail(err, "rescore");
+    e->d_rescore = e->rescore_buf.p;
     if ((err = hipMalloc(&e->d_work, 4 * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
     // fp64 scratch: log-mel + mfcc rows for the longest ring segment
     {
@@ -266,6 +284,7 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
             return bail(err, "block rms");
         if ((err = hipMalloc(&e->d_st, (size_t)n_streams * sizeof(GateStream))) != hipSuccess) return bail(err, "state");
         e->ev_cap = std::max(4096, 4 * n_streams);
+        if ((err = reserve_rescore(e, e->ev_cap)) != hipSuccess) return bail(err, "rescore list");
         if ((err = hipMalloc(&e->d_events, (size_t)e->ev_cap * sizeof(ewk_event))) != hipSuccess)
             return bail(err, "events");
         if ((err = hipMalloc(&e->d_evc, 4 * sizeof(int32_t))) != hipSuccess) return bail(err, "event counters");
@@ -369,6 +388,7 @@ int ewk_score_segments_device(ewk_engine* e, const float* d_pcm, const int64_t* 
         return fail(EWK_ENOTEMPLATE, "No reference word set. Call set_reference() first.");
     if (e->has_tmpl && !d_score) return fail(EWK_EINVAL, "d_score is required when a template is set");
     HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(reserve_rescore(e, n_seg));
     hipStream_t s = stream ? (hipStream_t)stream : e->stream;
     return score_linear(e, d_pcm, d_offsets, d_lengths, n_seg, d_mean, d_std, d_score, d_match, flags, s);
 }
@@ -405,6 +425,7 @@ int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int
         HIP_TRY(hipStreamSynchronize(e->stream));
         HIP_TRY(e->f64_scratch.reserve((size_t)per * e->f64_grid));
     }
+    HIP_TRY(reserve_rescore(e, n_seg));
     HIP_TRY(e->pcm.reserve(std::max<int64_t>(n_pcm, 1)));
     HIP_TRY(e->offsets.reserve(n_seg));
     HIP_TRY(e->lengths.reserve(n_seg));
@@ -560,12 +581,26 @@ static int push_impl(ewk_engine* e, const float* pcm, int64_t stride, int64_t ti
     const float* src = pcm;
     int64_t st_stride = stride, tk_stride = tick_stride;
     if (!(flags & EWK_PUSH_DEVICE)) {
+        // Gather the caller's (pageable) blocks into pinned staging on the CPU, then
+        // DMA asynchronously: the caller's buffer may die as soon as we return.
         const size_t per_stream = (size_t)n_ticks * e->cfg.block;
-        HIP_TRY(e->push_stage.reserve(per_stream * e->n_streams));
-        for (int32_t t = 0; t < n_ticks; ++t)
-            HIP_TRY(hipMemcpy2DAsync(e->push_stage.p + (size_t)t * e->cfg.block, per_stream * sizeof(float),
-                                     pcm + (size_t)t * tick_stride, stride * sizeof(float),
-                                     e->cfg.block * sizeof(float), e->n_streams, hipMemcpyHostToDevice, s));
+        const size_t total = per_stream * e->n_streams;
+        if (e->h_stage_free) HIP_TRY(hipEventSynchronize(e->h_stage_free));   // previous DMA done
+        if (total > e->h_stage_cap) {
+            if (e->h_stage) HIP_TRY(hipHostFree(e->h_stage));
+            e->h_stage = nullptr;
+            e->h_stage_cap = 0;
+            HIP_TRY(hipHostMalloc((void**)&e->h_stage, total * sizeof(float), hipHostMallocDefault));
+            e->h_stage_cap = total;
+        }
+        if (!e->h_stage_free) HIP_TRY(hipEventCreateWithFlags(&e->h_stage_free, hipEventDisableTiming));
+        for (int32_t st = 0; st < e->n_streams; ++st)
+            for (int32_t t = 0; t < n_ticks; ++t)
+                memcpy(e->h_stage + (size_t)st * per_stream + (size_t)t * e->cfg.block,
+                       pcm + (size_t)st * stride + (size_t)t * tick_stride, e->cfg.block * sizeof(float));
+        HIP_TRY(e->push_stage.reserve(total));
+        HIP_TRY(hipMemcpyAsync(e->push_stage.p, e->h_stage, total * sizeof(float), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipEventRecord(e->h_stage_free, s));
         src = e->push_stage.p;
         st_stride = (int64_t)per_stream;
         tk_stride = e->cfg.block;

@@ -50,6 +50,7 @@ constexpr int W_TILE = W_SCR + 4 * SCR_FRAME * 4;         // 16 x 130 floats
 constexpr int W_MISC = W_TILE + 16 * TILE_PITCH * 4;      // 64 floats
 constexpr int W_BYTES = ((W_MISC + 64 * 4) + 15) & ~15;
 constexpr int LDS_BYTES = L_SHARED_END + WAVES * W_BYTES;
+constexpr int kRescoreFrames = 16;
 static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU must fit");
 
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
@@ -445,7 +446,10 @@ __global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__
         const double score = a.cand_f32 ? score_f32cand(a.tmpl, a.tmpl + NMFCC, c32, c32 + NMFCC)
                                         : score_f64cand(a.tmpl, a.tmpl + NMFCC, c64, c64 + NMFCC);
         const int match = score >= a.threshold;
-        const bool near = fabs(score - a.threshold) < a.rescore_margin;
+        // fp64 re-score: decisions within the margin of the threshold, and very
+        // short segments (T <= kRescoreFrames) whose 2..16-frame std vectors are
+        // too ill-conditioned for the float32 pipeline to meet 1e-4.
+        const bool near = fabs(score - a.threshold) < a.rescore_margin || (1 + v.len / HOP) <= kRescoreFrames;
         if (RING) {
             a.events[seg].score = score;
             a.events[seg].match = match;
