@@ -20,7 +20,7 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   cd /tmp && export TMPDIR=/tmp
   R="${GRAFT_REPO_ROOT:-/root/repo}"
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "$R/gpurun_out/prof.log" 2>&1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline > "$R/gpurun_out/prof.log" 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -5 "$R/gpurun_out/prof.log"
   find "$R/gpurun_out/prof" -name "*stats*" | head
 fi
