@@ -13,7 +13,7 @@ import threading
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libewk.so")
+LIB_PATH = os.environ.get("EWK_LIB") or os.path.join(HERE, "libewk.so")
 
 N_MFCC = 20
 EWK_OK = 0

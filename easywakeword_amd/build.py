@@ -34,27 +34,30 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
+def build(force: bool = False, verbose: bool = False, out: str = None, defines=()) -> str:
+    """Compile every source for gfx950 and link libewk.so (or `out`)."""
+    lib = out or LIB
+    if out is None and not force and not needs_build():
         return LIB
     objs = []
     for src in SOURCES:
         obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
+        obj = obj + "".join(f".{d}" for d in defines).replace("=", "_")
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-               "-Wno-unused-function", "-c", os.path.join(CSRC, src), "-o", obj]
+               "-Wno-unused-function"] + [f"-D{d}" for d in defines] + ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
         objs.append(obj)
-    tmp = LIB + ".tmp"
+    tmp = lib + ".tmp"
     cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
+    os.replace(tmp, lib)
     for o in objs:
         os.remove(o)
-    return LIB
+    return lib
 
 
 if __name__ == "__main__":

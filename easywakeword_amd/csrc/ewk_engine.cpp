@@ -66,6 +66,7 @@ struct ewk_engine {
     Tables64* d_tab64 = nullptr;
     float* d_tmpl = nullptr;
     float h_tmpl[2 * NMFCC];
+    float uu_m32 = 0.f, uu_s32 = 0.f;   // numpy float32 dot of the template with itself
     bool has_tmpl = false;
 
     // rescoring
@@ -74,6 +75,7 @@ struct ewk_engine {
     int32_t* d_work = nullptr;      // scorer work counter
     int32_t rescore_cap = 4096;
     DevBuf<double> f64_scratch;
+    DevBuf<float2> lm_scratch;      // parked log-mel tiles, kLmTiles x 8 KB per scorer wave
     int f64_grid = 64;
 
     // host-API staging
@@ -151,6 +153,16 @@ static hipError_t reserve_rescore(ewk_engine* e, int32_t n_seg) {
     return hipSuccess;
 }
 
+// Size the per-wave log-mel scratch for a launch of `n_seg` segments.
+static hipError_t reserve_lm(ewk_engine* e, int32_t n_seg, int ring_mode) {
+    const size_t waves = (size_t)score_grid(n_seg, ring_mode) * WAVES;
+    const size_t need = waves * kLmTiles * 16 * 64;
+    if (need <= e->lm_scratch.cap) return hipSuccess;
+    hipError_t err = hipStreamSynchronize(e->stream);
+    if (err != hipSuccess) return err;
+    return e->lm_scratch.reserve(need);
+}
+
 extern "C" {
 
 void ewk_default_config(ewk_config* c) {
@@ -191,6 +203,7 @@ void ewk_destroy(ewk_engine* e) {
     e->rescore_buf.release();
     (void)hipFree(e->d_work);
     e->f64_scratch.release();
+    e->lm_scratch.release();
     e->pcm.release();
     e->offsets.release();
     e->lengths.release();
@@ -254,9 +267,9 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
         std::vector<unsigned char> buf(sizeof(Tables));
         Tables* t = reinterpret_cast<Tables*>(buf.data());
         build_tables(t);
-        if (t->melw_count > MELW_CAP) {
+        if (!t->ok) {
             ewk_destroy(e);
-            return fail(EWK_EHIP, "mel table overflow");
+            return fail(EWK_EHIP, "mel filterbank does not fit the kernel's band layout");
         }
         if ((err = hipMalloc(&e->d_tab, sizeof(Tables))) != hipSuccess) return bail(err, "tables");
         if ((err = hipMemcpy(e->d_tab, t, sizeof(Tables), hipMemcpyHostToDevice)) != hipSuccess) return bail(err, "tables");
@@ -285,6 +298,7 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
         if ((err = hipMalloc(&e->d_st, (size_t)n_streams * sizeof(GateStream))) != hipSuccess) return bail(err, "state");
         e->ev_cap = std::max(4096, 4 * n_streams);
         if ((err = reserve_rescore(e, e->ev_cap)) != hipSuccess) return bail(err, "rescore list");
+        if ((err = reserve_lm(e, e->ev_cap, 1)) != hipSuccess) return bail(err, "log-mel scratch");
         if ((err = hipMalloc(&e->d_events, (size_t)e->ev_cap * sizeof(ewk_event))) != hipSuccess)
             return bail(err, "events");
         if ((err = hipMalloc(&e->d_evc, 4 * sizeof(int32_t))) != hipSuccess) return bail(err, "event counters");
@@ -313,6 +327,16 @@ int ewk_set_template(ewk_engine* e, const float* mean20, const float* std20) {
     if (!e || !mean20 || !std20) return fail(EWK_EINVAL, "NULL argument");
     memcpy(e->h_tmpl, mean20, NMFCC * sizeof(float));
     memcpy(e->h_tmpl + NMFCC, std20, NMFCC * sizeof(float));
+    {   // cblas_sdot for n = 20: float products accumulated in double, rounded to float
+        double am = 0.0, as = 0.0;
+        for (int i = 0; i < NMFCC; ++i) {
+            const float pm = mean20[i] * mean20[i], ps = std20[i] * std20[i];
+            am += (double)pm;
+            as += (double)ps;
+        }
+        e->uu_m32 = (float)am;
+        e->uu_s32 = (float)as;
+    }
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipMemcpyAsync(e->d_tmpl, e->h_tmpl, sizeof(e->h_tmpl), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
@@ -340,12 +364,16 @@ static ScoreArgs base_args(ewk_engine* e) {
     memset(&a, 0, sizeof(a));
     a.has_template = e->has_tmpl ? 1 : 0;
     a.tmpl = e->d_tmpl;
+    a.uu_m32 = e->uu_m32;
+    a.uu_s32 = e->uu_s32;
     a.threshold = e->cfg.similarity_threshold;
     a.rescore_margin = e->cfg.rescore_margin;
     a.rescore_count = e->d_rescore;
     a.rescore_list = e->d_rescore + 1;
     a.rescore_cap = e->rescore_cap;
     a.work = e->d_work;
+    a.lm_scratch = e->lm_scratch.p;
+    a.lm_tiles = kLmTiles;
     return a;
 }
 
@@ -389,6 +417,7 @@ int ewk_score_segments_device(ewk_engine* e, const float* d_pcm, const int64_t* 
     if (e->has_tmpl && !d_score) return fail(EWK_EINVAL, "d_score is required when a template is set");
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(reserve_rescore(e, n_seg));
+    HIP_TRY(reserve_lm(e, n_seg, 0));
     hipStream_t s = stream ? (hipStream_t)stream : e->stream;
     return score_linear(e, d_pcm, d_offsets, d_lengths, n_seg, d_mean, d_std, d_score, d_match, flags, s);
 }
@@ -426,6 +455,7 @@ int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int
         HIP_TRY(e->f64_scratch.reserve((size_t)per * e->f64_grid));
     }
     HIP_TRY(reserve_rescore(e, n_seg));
+    HIP_TRY(reserve_lm(e, n_seg, 0));
     HIP_TRY(e->pcm.reserve(std::max<int64_t>(n_pcm, 1)));
     HIP_TRY(e->offsets.reserve(n_seg));
     HIP_TRY(e->lengths.reserve(n_seg));

@@ -16,7 +16,7 @@ constexpr int HOP = 160;
 constexpr int NBIN = NFFT / 2 + 1;   // 257
 constexpr int NMEL = 128;
 constexpr int NMFCC = EWK_N_MFCC;    // 20
-constexpr int MELW_CAP = 768;        // packed non-zero Slaney weights (~520 used)
+constexpr int MEL_ITERS = 40;        // unrolled mel FMAs per lane: sum of per-group band widths
 constexpr int DCT_PITCH = 130;       // LDS row pitch of the DCT table (bank-conflict free A reads)
 constexpr int TILE_PITCH = 130;      // LDS row pitch of the per-wave log-mel tile
 constexpr int SCR_FRAME = 272;       // per-frame FFT scratch floats (16 rows x 17)
@@ -28,12 +28,11 @@ struct Tables {
     float2 tw1[256];         // [k1*16 + j] = exp(-2*pi*i*j*k1/256)
     float2 tw2[256];         // [k]  = (cos, sin)(2*pi*k/512) for the real-FFT untangle
     int32_t band_lo[NMEL];   // first non-zero bin of mel band m
-    int32_t band_n[NMEL];    // number of non-zero bins of band m
-    int32_t band_off[NMEL];  // offset of band m in melw
-    float melw[MELW_CAP];    // 0.25 * librosa float32 weights (0.25 folds the untangle's 1/2 squared)
+    // 0.25 * librosa float32 weights (0.25 folds the untangle's 1/2 squared), laid
+    // out [iteration][lane j] for band m = j + 16*i, zero-padded to the group width
+    float wpad[MEL_ITERS * 16];
     float dct[NMFCC * NMEL]; // DCT-II ortho rows 0..19
-    int32_t melw_count;
-    int32_t pad[3];
+    int32_t ok;              // every band fits its compile-time group width
 };
 
 // fp64 path tables (rescoring / reference precision).
@@ -64,6 +63,7 @@ struct ScoreArgs {
     int32_t has_template;
     int32_t cand_f32;         // candidate dtype of the reference path: 1 float32, 0 float64
     const float* tmpl;        // [40] template mean[20], std[20]
+    float uu_m32, uu_s32;     // template self-dots as numpy computes them (float32 sdot)
     float* out_mean;
     float* out_std;
     double* out_score;
@@ -73,12 +73,18 @@ struct ScoreArgs {
     int32_t* rescore_list;    // indices whose fp32 score fell inside the margin
     int32_t* rescore_count;
     int32_t rescore_cap;
+    float2* lm_scratch;       // per-wave parked log-mel tiles for the top_db clamp pass
+    int32_t lm_tiles;         // tiles per wave in lm_scratch
 };
 
 hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mode, hipStream_t s);
 // ring mode: *ev_base = *n_events after a scoring pass
 hipError_t launch_advance_watermark(int32_t* ev_base, const int32_t* n_events, hipStream_t s);
 constexpr int kScoreGridMax = 512;   // 2 workgroups x 256 CUs: one resident wave of the grid
+constexpr int kScoreGridRing = 256;  // ring-mode grid (device-side event count)
+int score_grid(int n_seg, int ring_mode);
+// log-mel tiles parked per wave for the top_db pass: segments up to 3 s (T <= 301)
+constexpr int kLmTiles = (1 + 48000 / HOP + 15) / 16;
 // fp64 re-score of rescore_list (device count) or of all n (list == nullptr).
 hipError_t launch_score_f64(const Tables64* d_tab64, const ScoreArgs& a, int ring_mode,
                             double* d_scratch, int64_t scratch_per_seg, int grid,

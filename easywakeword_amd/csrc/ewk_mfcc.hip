@@ -6,30 +6,42 @@
 // feature.mfcc(n_mfcc=20, n_fft=512, hop=160) + scipy cosine + the score
 // scaling, for many segments per launch.
 //
-// Design (one wave = one segment; 4 waves per workgroup share the tables):
+// Design (one wave = one segment; 4 waves per workgroup share the tables;
+// a persistent grid pulls segments from an atomic work counter):
 //   frames  : stft(center=True, pad_mode=constant): frame t covers samples
 //             [t*160-256, t*160+256) of the segment, zero outside; T = 1+L//160.
-//   FFT     : 16 lanes per frame, 4 frames per wave-pass.  The 512-point real
+//   staging : the 4 frames of a wave pass span 992 contiguous samples; they are
+//             loaded one pass ahead with coalesced dword loads (bounds / ring wrap
+//             resolved once per sample) and parked in LDS.
+//   FFT     : 16 lanes per frame, 4 frames per wave pass.  The 512-point real
 //             frame is packed as 256 complex points z[n] = x[2n] + i x[2n+1];
 //             256 = 16 x 16 four-step FFT: a register DFT16 per lane, a
 //             twiddle, an LDS transpose, a second register DFT16, then the
 //             real-FFT untangle X[k] = (Z[k]+Z*[256-k])/2 - i W512^k (Z[k]-Z*[256-k])/2.
-//   mel     : sparse Slaney filterbank from LDS (<=2 filters per bin), then
-//             10*log10(max(1e-10, .)); written to a 16-frame log-mel tile.
+//   mel     : Slaney bands from LDS, fully unrolled with compile-time group
+//             widths (band m = j + 16 i; widths {2,2,2,3,4,6,9,12} cover every
+//             band, weights zero-padded), then 10*log10(max(1e-10, .)) via
+//             v_log_f32; written to a 16-frame log-mel tile.
 //   DCT     : the only dense GEMM on the path: C[32 x 16] = D[32 x 128] . X[128 x 16]
 //             per 16-frame tile on the matrix cores (v_mfma_f32_16x16x4_f32, exact
 //             f32 fma chains), rows 20..31 zero.
 //   top_db  : power_to_db clamps at (segment max - 80 dB), a segment-global
-//             coupling.  Pass 1 assumes no clamp and tracks the log-mel max/min;
-//             if min < max-80 the segment is recomputed with the clamp (pass 2).
+//             coupling.  Pass 1 computes the unclamped DCT, tracks the log-mel
+//             max/min and parks every log-mel tile in a per-wave global scratch;
+//             if min < max-80, pass 2 re-reads the tiles, clamps and redoes only
+//             the DCT + statistics (no FFT).
 //   stats   : population mean/std over frames from fp64 shifted sums
 //             (d = c - c[frame 0]) -- exact 0 std for identical frames.
-//   score   : fp64 cosine of the fp32-rounded stats against the fp32 template,
-//             0.7/0.3 blend, x100, p**1.5/10 (wakeword.py:611-625); NaN kept.
+//   score   : the reference's own float32 / float64 cosine arithmetic
+//             (wakeword.py:611-625 + scipy correlation); NaN kept.
 #include <hip/hip_runtime.h>
 #include <math.h>
 
 #include "ewk_internal.h"
+
+#ifndef EWK_ABLATE
+#define EWK_ABLATE 0   // timing-only ablations (scripts/mb_score.py); 0 in every real build
+#endif
 
 namespace ewk {
 
@@ -40,18 +52,18 @@ constexpr int L_WIN2 = 0;
 constexpr int L_TW1 = L_WIN2 + 256 * 8;
 constexpr int L_TW2 = L_TW1 + 256 * 8;
 constexpr int L_BLO = L_TW2 + 256 * 8;
-constexpr int L_BN = L_BLO + NMEL * 4;
-constexpr int L_BOFF = L_BN + NMEL * 4;
-constexpr int L_MELW = L_BOFF + NMEL * 4;
-constexpr int L_DCT = L_MELW + MELW_CAP * 4;
+constexpr int L_WPAD = L_BLO + NMEL * 4;
+constexpr int L_DCT = L_WPAD + MEL_ITERS * 16 * 4;
 constexpr int L_SHARED_END = ((L_DCT + NMFCC * DCT_PITCH * 4) + 15) & ~15;
-constexpr int W_SCR = 0;                                  // 4 frames x 272 floats
+constexpr int W_SCR = 0;                                  // 4 frames x 272 floats (also the sample staging)
 constexpr int W_TILE = W_SCR + 4 * SCR_FRAME * 4;         // 16 x 130 floats
 constexpr int W_MISC = W_TILE + 16 * TILE_PITCH * 4;      // 64 floats
 constexpr int W_BYTES = ((W_MISC + 64 * 4) + 15) & ~15;
 constexpr int LDS_BYTES = L_SHARED_END + WAVES * W_BYTES;
 constexpr int kRescoreFrames = 16;
+constexpr int kStage = 1024;                              // staged samples per pass (>= 3*160 + 512)
 static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU must fit");
+static_assert(kStage <= 4 * SCR_FRAME, "staging must fit the FFT scratch");
 
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 
@@ -93,8 +105,8 @@ __device__ __forceinline__ void dft16_perm(float2 (&x)[16]) {
 __device__ __forceinline__ constexpr int dperm(int k) { return 4 * (k & 3) + (k >> 2); }
 
 struct SegView {
-    const float* p;   // stream ring base or linear pcm base
-    int64_t start;
+    const float* p;   // linear: segment base; ring: stream ring base
+    int64_t start;    // ring: physical index of sample 0
     int64_t ring;     // 0 = linear
     int32_t len;
 };
@@ -106,40 +118,74 @@ __device__ __forceinline__ float seg_sample(const SegView& v, int q) {
     return v.p[idx];
 }
 
-// One 4-frame pass: frames t0 + (lane>>4).  Writes rows [row0, row0+4) of the
-// log-mel tile.  Returns per-lane max/min of the valid log-mel values.
-__device__ __forceinline__ void frame_pass(const SegView& v, int t0, int T, int row0, bool clamp, float theta,
+// Coalesced staging loads: lane l fetches samples q0 + 64*c + l, c = 0..15.
+__device__ __forceinline__ void stage_load(const SegView& v, int q0, int lane, float (&r)[16]) {
+    const float* base = v.p + v.start;            // linear: segment start; ring: wraps below
+    const int ring = (int)v.ring;
+    const int wrap_at = ring ? ring - (int)v.start : 0x7fffffff;   // q >= wrap_at -> q - ring
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const int q = q0 + 64 * c + lane;
+        const bool in = (unsigned)q < (unsigned)v.len;
+#if EWK_ABLATE & 1
+        r[c] = in ? (float)((q * 7) & 255) * 1e-3f : 0.0f;
+#else
+        const int off = q >= wrap_at ? q - ring : q;
+        r[c] = in ? base[off] : 0.0f;
+#endif
+    }
+}
+
+__device__ __forceinline__ void stage_store(float* stage, int lane, const float (&r)[16]) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c) stage[64 * c + lane] = r[c];
+}
+
+constexpr int kMelW[8] = {2, 2, 2, 3, 4, 6, 9, 12};   // per 16-band group (checked on the host)
+
+// One 4-frame pass: frames t0 + (lane>>4), samples already staged in `scr`.
+// Writes rows [row0, row0+4) of the log-mel tile (invalid frames -> 0) and
+// returns the per-lane max/min of the valid log-mel values.  If `next` is
+// set, the next pass's samples are fetched meanwhile and staged at the end.
+__device__ __forceinline__ void frame_pass(const SegView& v, int t0, int T, int row0, bool next,
                                            const unsigned char* smem, float* scr, float* tile,
                                            int lane, float& vmax, float& vmin) {
     const float2* s_win2 = reinterpret_cast<const float2*>(smem + L_WIN2);
     const float2* s_tw1 = reinterpret_cast<const float2*>(smem + L_TW1);
     const float2* s_tw2 = reinterpret_cast<const float2*>(smem + L_TW2);
     const int* s_blo = reinterpret_cast<const int*>(smem + L_BLO);
-    const int* s_bn = reinterpret_cast<const int*>(smem + L_BN);
-    const int* s_boff = reinterpret_cast<const int*>(smem + L_BOFF);
-    const float* s_melw = reinterpret_cast<const float*>(smem + L_MELW);
+    const float* s_wpad = reinterpret_cast<const float*>(smem + L_WPAD);
 
     const int f = lane >> 4, j = lane & 15;
     const int t = t0 + f;
     const bool valid = t < T;
     float* sc = scr + f * SCR_FRAME;
 
-    // ---- load + window: lane j holds z[16*n1 + j] = x[32*n1+2j] + i x[32*n1+2j+1]
+    // ---- window the staged samples: lane j holds z[16*n1 + j] = x[32*n1+2j] + i x[32*n1+2j+1]
     float2 a[16];
-    const int qbase = t * HOP - NFFT / 2 + 2 * j;
+    {
+        const float2* st2 = reinterpret_cast<const float2*>(scr + f * HOP + 2 * j);
 #pragma unroll
-    for (int n1 = 0; n1 < 16; ++n1) {
-        const int q = qbase + 32 * n1;
-        const float x0 = seg_sample(v, q), x1 = seg_sample(v, q + 1);
-        const float2 w = s_win2[16 * n1 + j];
-        a[n1] = make_float2(x0 * w.x, x1 * w.y);
+        for (int n1 = 0; n1 < 16; ++n1) {
+            const float2 x = st2[16 * n1];
+            const float2 w = s_win2[16 * n1 + j];
+            a[n1] = make_float2(x.x * w.x, x.y * w.y);
+        }
     }
+    lds_order();
+    // ---- prefetch the next pass while this one computes
+    float pf[16];
+    if (next) stage_load(v, (t0 + 4) * HOP - NFFT / 2, lane, pf);
     // ---- DFT16 over n1, twiddle W256^(j*k1)
     dft16_perm(a);
 #pragma unroll
     for (int k1 = 1; k1 < 16; ++k1) a[dperm(k1)] = cmul(a[dperm(k1)], s_tw1[k1 * 16 + j]);
     // ---- transpose through LDS (real, then imaginary half): lane k1 <- A_{n2}[k1]
     float2 b[16];
+#if EWK_ABLATE & 2
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) b[k1] = a[dperm(k1)];
+#else
 #pragma unroll
     for (int k1 = 0; k1 < 16; ++k1) sc[k1 * 17 + j] = a[dperm(k1)].x;
     lds_order();
@@ -152,10 +198,15 @@ __device__ __forceinline__ void frame_pass(const SegView& v, int t0, int T, int 
 #pragma unroll
     for (int n2 = 0; n2 < 16; ++n2) b[n2].y = sc[j * 17 + n2];
     lds_order();
+#endif
     // ---- DFT16 over n2: Z[j + 16*k2] = b[dperm(k2)]
     dft16_perm(b);
     // ---- untangle: partner Z[(256-k) & 255], k = j + 16*k2
     float2 zp[16];
+#if EWK_ABLATE & 2
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) zp[k2] = b[dperm(15 - k2)];
+#else
 #pragma unroll
     for (int k2 = 0; k2 < 16; ++k2) sc[j + 16 * k2] = b[dperm(k2)].x;
     lds_order();
@@ -168,6 +219,7 @@ __device__ __forceinline__ void frame_pass(const SegView& v, int t0, int T, int 
 #pragma unroll
     for (int k2 = 0; k2 < 16; ++k2) zp[k2].y = sc[(256 - (j + 16 * k2)) & 255];
     lds_order();
+#endif
     // P'[k] = |2 X[k]|^2 = |A - i W512^k B|^2, A = Z[k] + conj(Zp), B = Z[k] - conj(Zp)
     float pw[16];
 #pragma unroll
@@ -188,80 +240,82 @@ __device__ __forceinline__ void frame_pass(const SegView& v, int t0, int T, int 
     }
 #pragma unroll
     for (int k2 = 0; k2 < 16; ++k2) sc[j + 16 * k2] = pw[k2];
-    if (j == 0) sc[256] = p256;
+    // bin 256 and the zero pad the unrolled band loops read past it
+    sc[256 + j] = (j == 0) ? p256 : 0.0f;
     lds_order();
     // ---- mel + log: lane j computes bands m = j + 16*i of its frame
     float* trow = tile + (row0 + f) * TILE_PITCH;
-#pragma unroll 2
+    int it = 0;
+#pragma unroll
     for (int i = 0; i < 8; ++i) {
         const int m = j + 16 * i;
-        const int lo = s_blo[m], n = s_bn[m], off = s_boff[m];
+        const int lo = s_blo[m];
         float acc = 0.0f;
-        for (int q = 0; q < n; ++q) acc = fmaf(s_melw[off + q], sc[lo + q], acc);
-        float db = 10.0f * log10f(fmaxf(1e-10f, acc));
+#if EWK_ABLATE & 4
+        acc = s_wpad[it * 16 + j] * sc[lo] + 1.0f;
+#else
+#pragma unroll
+        for (int q = 0; q < kMelW[i]; ++q) acc = fmaf(s_wpad[(it + q) * 16 + j], sc[lo + q], acc);
+#endif
+        it += kMelW[i];
+#if EWK_ABLATE & 8
+        float db = acc;
+#else
+        // 10*log10(x) = (10*log10(2)) * log2(x), v_log_f32
+        float db = 3.0102999566398120f * __log2f(fmaxf(1e-10f, acc));
+#endif
         if (valid) {
             vmax = fmaxf(vmax, db);
             vmin = fminf(vmin, db);
         }
-        if (clamp) db = fmaxf(db, theta);
         trow[m] = valid ? db : 0.0f;
     }
     lds_order();
+    if (next) stage_store(scr, lane, pf);
+    lds_order();
 }
 
-// Whole-segment pipeline for one wave.  On return lanes with (lane&15)==0 hold
-// the fp64 sums for coefficients (16*rt + 4*(lane>>4) + r).
-__device__ void segment_stats(const SegView& v, const unsigned char* smem, float* scr, float* tile,
-                              int lane, bool clamp, float theta,
-                              double (&s1)[8], double (&s2)[8], float& vmax, float& vmin) {
-    const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
-    const int T = 1 + v.len / HOP;
-    const int ntile = (T + 15) >> 4;
+// DCT of one 16-frame log-mel tile on the matrix cores + fp64 statistics update.
+// Lane l holds C[row = 4h + r][frame col] of both row tiles (h = l>>4, col = l&15).
+__device__ __forceinline__ void tile_dct_stats(const float* tile, const float* s_dct, int tile_i, int T,
+                                               int lane, float (&cref)[8], double (&s1)[8], double (&s2)[8]) {
     const int col = lane & 15, h = lane >> 4;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; }
-    float cref[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) cref[i] = 0.0f;
-    vmax = -INFINITY;
-    vmin = INFINITY;
-    for (int tile_i = 0; tile_i < ntile; ++tile_i) {
-#pragma unroll 1
-        for (int p = 0; p < 4; ++p)
-            frame_pass(v, tile_i * 16 + p * 4, T, p * 4, clamp, theta, smem, scr, tile, lane, vmax, vmin);
-        // DCT on the matrix cores: two 16-row tiles (rows 0..15, 16..31; 20..31 are zero)
-        floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-        const float* brow = tile + col * TILE_PITCH + h;
-        const float* arow0 = s_dct + col * DCT_PITCH + h;
-        const float* arow1 = s_dct + (16 + (col & 3)) * DCT_PITCH + h;
-        const bool a1ok = col < 4;
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    const float* brow = tile + col * TILE_PITCH + h;
+    const float* arow0 = s_dct + col * DCT_PITCH + h;
+    const float* arow1 = s_dct + (16 + (col & 3)) * DCT_PITCH + h;
+    const bool a1ok = col < 4;
 #pragma unroll 8
-        for (int s = 0; s < 32; ++s) {
-            const float bv = brow[4 * s];
-            const float a0 = arow0[4 * s];
-            const float a1 = a1ok ? arow1[4 * s] : 0.0f;
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bv, acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bv, acc1, 0, 0, 0);
-        }
-        lds_order();
-        // lane holds C[row = 4h + r][frame col] for both row tiles
-        float c[8] = {acc0[0], acc0[1], acc0[2], acc0[3], acc1[0], acc1[1], acc1[2], acc1[3]};
-        if (tile_i == 0) {
+    for (int s = 0; s < 32; ++s) {
+        const float bv = brow[4 * s];
+        const float a0 = arow0[4 * s];
+        const float a1 = a1ok ? arow1[4 * s] : 0.0f;
+#if EWK_ABLATE & 16
+        acc0[s & 3] += a0 * bv;
+        acc1[s & 3] += a1 * bv;
+#else
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bv, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bv, acc1, 0, 0, 0);
+#endif
+    }
+    lds_order();
+    float c[8] = {acc0[0], acc0[1], acc0[2], acc0[3], acc1[0], acc1[1], acc1[2], acc1[3]};
+    if (tile_i == 0) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
-        }
-        const bool fvalid = tile_i * 16 + col < T;
-        if (fvalid) {
+        for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
+    }
+    if (tile_i * 16 + col < T) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const double d = (double)c[i] - (double)cref[i];
-                s1[i] += d;
-                s2[i] = fma(d, d, s2[i]);
-            }
+        for (int i = 0; i < 8; ++i) {
+            const double d = (double)c[i] - (double)cref[i];
+            s1[i] += d;
+            s2[i] = fma(d, d, s2[i]);
         }
     }
-    // reduce over the 16 frame columns (xor 1,2,4,8 stays inside a 16-lane row),
-    // then mean = cref + s1/T, var = (s2 - s1^2/T)/T  (returned in s1 / s2)
+}
+
+// Reduce the per-lane sums over the 16 frame columns; returns mean in s1 and std in s2.
+__device__ __forceinline__ void finish_stats(int T, const float (&cref)[8], double (&s1)[8], double (&s2)[8]) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -276,12 +330,105 @@ __device__ void segment_stats(const SegView& v, const unsigned char* smem, float
         s1[i] = mean;
         s2[i] = sqrt(var);
     }
+}
+
+// Whole segment for one wave.  gscr: this wave's log-mel scratch ([tile][16][64] float2),
+// able to hold `scr_tiles` tiles.
+__device__ void segment_stats(const SegView& v, const unsigned char* smem, float* scr, float* tile,
+                              float2* gscr, int scr_tiles, int lane, double (&s1)[8], double (&s2)[8]) {
+    const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
+    const int T = 1 + v.len / HOP;
+    const int ntile = (T + 15) >> 4;
+    const int npass = (T + 3) >> 2;
+    const bool park = ntile <= scr_tiles;
+    float cref[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
+    float vmax = -INFINITY, vmin = INFINITY;
+    {   // stage the first pass synchronously
+        float r[16];
+        stage_load(v, -NFFT / 2, lane, r);
+        stage_store(scr, lane, r);
+        lds_order();
+    }
+    // tile copy mapping: lane l owns row l>>2, columns (l&3)*32 .. +32 as 16 float2
+    const int crow = lane >> 2, ccol = (lane & 3) * 32;
+    for (int tile_i = 0; tile_i < ntile; ++tile_i) {
+#pragma unroll 1
+        for (int p = 0; p < 4; ++p) {
+            const int pass = tile_i * 4 + p;
+            if (pass < npass)
+                frame_pass(v, pass * 4, T, p * 4, pass + 1 < npass, smem, scr, tile, lane, vmax, vmin);
+            else {   // rows of frames past T: zero (ignored by the statistics)
+                for (int m = lane & 15; m < NMEL; m += 16) tile[(p * 4 + (lane >> 4)) * TILE_PITCH + m] = 0.0f;
+            }
+        }
+        lds_order();
+        if (park) {
+            const float2* src = reinterpret_cast<const float2*>(tile + crow * TILE_PITCH + ccol);
+            float2* dst = gscr + (int64_t)tile_i * 16 * 64 + lane;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) dst[k * 64] = src[k];
+        }
+        tile_dct_stats(tile, s_dct, tile_i, T, lane, cref, s1, s2);
+    }
     // wave-wide log-mel max/min
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) {
         vmax = fmaxf(vmax, __shfl_xor(vmax, m, 64));
         vmin = fminf(vmin, __shfl_xor(vmin, m, 64));
     }
+    const float theta = vmax - 80.0f;
+#if !(EWK_ABLATE & 32)
+    if (vmin < theta) {
+        // top_db clamp: redo the DCT + statistics from the parked log-mel tiles
+#pragma unroll
+        for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; }
+        if (park) {
+            float2 nx[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) nx[k] = gscr[k * 64 + lane];
+            for (int tile_i = 0; tile_i < ntile; ++tile_i) {
+                float2* dst = reinterpret_cast<float2*>(tile + crow * TILE_PITCH + ccol);
+#pragma unroll
+                for (int k = 0; k < 16; ++k) dst[k] = make_float2(fmaxf(nx[k].x, theta), fmaxf(nx[k].y, theta));
+                lds_order();
+                if (tile_i + 1 < ntile) {   // next tile's loads overlap this tile's MFMAs
+                    const float2* src = gscr + (int64_t)(tile_i + 1) * 16 * 64 + lane;
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) nx[k] = src[k * 64];
+                }
+                tile_dct_stats(tile, s_dct, tile_i, T, lane, cref, s1, s2);
+            }
+        } else {
+            // longer than the scratch: recompute the FFT with the clamp applied per tile
+            {
+                float r[16];
+                stage_load(v, -NFFT / 2, lane, r);
+                stage_store(scr, lane, r);
+                lds_order();
+            }
+            float d0 = 0.f, d1 = 0.f;
+            for (int tile_i = 0; tile_i < ntile; ++tile_i) {
+#pragma unroll 1
+                for (int p = 0; p < 4; ++p) {
+                    const int pass = tile_i * 4 + p;
+                    if (pass < npass)
+                        frame_pass(v, pass * 4, T, p * 4, pass + 1 < npass, smem, scr, tile, lane, d0, d1);
+                    else
+                        for (int m = lane & 15; m < NMEL; m += 16) tile[(p * 4 + (lane >> 4)) * TILE_PITCH + m] = 0.0f;
+                }
+                lds_order();
+                float* trow = tile + crow * TILE_PITCH + ccol;
+#pragma unroll
+                for (int k = 0; k < 32; ++k) trow[k] = fmaxf(trow[k], theta);
+                lds_order();
+                tile_dct_stats(tile, s_dct, tile_i, T, lane, cref, s1, s2);
+            }
+        }
+    }
+#endif
+    finish_stats(T, cref, s1, s2);
 }
 
 // ---- the score, exactly as WordMatcher.calculate_similarity evaluates it --------
@@ -358,6 +505,32 @@ __device__ double score_f32cand(const float* tm, const float* ts, const float* c
     return (double)(powf(percent, 1.5f) / 10.0f);
 }
 
+__device__ __forceinline__ double wave_sum_d(double x) {
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) x += __shfl_xor(x, m, 64);
+    return x;
+}
+
+// Fast-path finishes (the fp64 re-score keeps the reference's exact pow / sequential dots).
+__device__ __forceinline__ double score_f64_finish(double uu_m, double uu_s, double uv_m, double vv_m, double uv_s,
+                                                   double vv_s) {
+#pragma clang fp contract(off)
+    const double sm = 1.0 - clip02(1.0 - uv_m / sqrt(uu_m * vv_m));
+    const double ss = 1.0 - clip02(1.0 - uv_s / sqrt(uu_s * vv_s));
+    const double percent = (sm * 0.7 + ss * 0.3) * 100.0;
+    return percent * sqrt(percent) / 10.0;   // p**1.5 (NaN for p < 0 like pow)
+}
+
+__device__ __forceinline__ double score_f32_finish(float uu_m, float uu_s, float uv_m, float vv_m, float uv_s,
+                                                   float vv_s) {
+#pragma clang fp contract(off)
+    const float dm = clip02f(1.0f - uv_m / (float)sqrt((double)(uu_m * vv_m)));
+    const float ds = clip02f(1.0f - uv_s / (float)sqrt((double)(uu_s * vv_s)));
+    const float combined = (1.0f - dm) * 0.7f + (1.0f - ds) * 0.3f;
+    const float percent = combined * 100.0f;
+    return (double)(powf(percent, 1.5f) / 10.0f);
+}
+
 template <int RING>
 __global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__ tab, ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -368,9 +541,9 @@ __global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__
         // win2, tw1, tw2 are contiguous at the start of Tables (3 * 2048 B)
         for (int i = threadIdx.x; i < 3 * 2048 / 16; i += blockDim.x) s[i] = g[i];
         int* sb = reinterpret_cast<int*>(smem + L_BLO);
-        for (int i = threadIdx.x; i < 3 * NMEL; i += blockDim.x) sb[i] = tab->band_lo[i];  // lo,n,off contiguous
-        float* sw = reinterpret_cast<float*>(smem + L_MELW);
-        for (int i = threadIdx.x; i < MELW_CAP; i += blockDim.x) sw[i] = tab->melw[i];
+        for (int i = threadIdx.x; i < NMEL; i += blockDim.x) sb[i] = tab->band_lo[i];
+        float* sw = reinterpret_cast<float*>(smem + L_WPAD);
+        for (int i = threadIdx.x; i < MEL_ITERS * 16; i += blockDim.x) sw[i] = tab->wpad[i];
         float* sd = reinterpret_cast<float*>(smem + L_DCT);
         for (int i = threadIdx.x; i < NMFCC * NMEL; i += blockDim.x)
             sd[(i / NMEL) * DCT_PITCH + (i % NMEL)] = tab->dct[i];
@@ -386,83 +559,86 @@ __global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__
     float* scr = reinterpret_cast<float*>(wbase + W_SCR);
     float* tile = reinterpret_cast<float*>(wbase + W_TILE);
     float* misc = reinterpret_cast<float*>(wbase + W_MISC);
+    float2* gscr = a.lm_scratch + (int64_t)(blockIdx.x * WAVES + wave) * a.lm_tiles * 16 * 64;
     // persistent waves pull segments from a work counter (ragged lengths balance)
     for (;;) {
-    int idx = 0;
-    if (lane == 0) idx = atomicAdd(a.work, 1);
-    idx = __shfl(idx, 0, 64);
-    if (idx >= count) break;
-    const int seg = base + idx;
+        int idx = 0;
+        if (lane == 0) idx = atomicAdd(a.work, 1);
+        idx = __shfl(idx, 0, 64);
+        if (idx >= count) break;
+        const int seg = base + idx;
 
-    SegView v;
-    if (RING) {
-        const ewk_event ev = a.events[seg];
-        v.p = a.pcm + (int64_t)ev.stream * a.ring_len;
-        v.start = ev.ring_start;
-        v.ring = a.ring_len;
-        v.len = ev.length;
-        if (ev.flags & EWK_EV_SKIPPED) continue;
-    } else {
-        v.p = a.pcm;
-        v.start = a.offsets[seg];
-        v.ring = 0;
-        v.len = a.lengths[seg];
-    }
+        SegView v;
+        if (RING) {
+            const ewk_event ev = a.events[seg];
+            v.p = a.pcm + (int64_t)ev.stream * a.ring_len;
+            v.start = ev.ring_start;
+            v.ring = a.ring_len;
+            v.len = ev.length;
+            if (ev.flags & EWK_EV_SKIPPED) continue;
+        } else {
+            v.p = a.pcm;
+            v.start = a.offsets[seg];
+            v.ring = 0;
+            v.len = a.lengths[seg];
+        }
 
-    double st1[8], st2[8];
-    float vmax, vmin;
-    segment_stats(v, smem, scr, tile, lane, false, 0.0f, st1, st2, vmax, vmin);
-    const float theta = vmax - 80.0f;
-    if (vmin < theta) segment_stats(v, smem, scr, tile, lane, true, theta, st1, st2, vmax, vmin);
+        double st1[8], st2[8];
+        segment_stats(v, smem, scr, tile, gscr, a.lm_tiles, lane, st1, st2);
 
-    // ---- gather fp32-rounded mean/std into misc[0..19], misc[20..39]
-    if ((lane & 15) == 0) {
-        const int h = lane >> 4;
+        // ---- gather fp32-rounded mean/std into misc[0..19], misc[20..39]
+        if ((lane & 15) == 0) {
+            const int h = lane >> 4;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            misc[4 * h + r] = (float)st1[r];
-            misc[20 + 4 * h + r] = (float)st2[r];
-            if (h == 0) {
-                misc[16 + r] = (float)st1[4 + r];
-                misc[36 + r] = (float)st2[4 + r];
+            for (int r = 0; r < 4; ++r) {
+                misc[4 * h + r] = (float)st1[r];
+                misc[20 + 4 * h + r] = (float)st2[r];
+                if (h == 0) {
+                    misc[16 + r] = (float)st1[4 + r];
+                    misc[36 + r] = (float)st2[4 + r];
+                }
             }
         }
-    }
-    lds_order();
-    float cm = 0.0f, cs = 0.0f;
-    if (lane < NMFCC) {
-        cm = misc[lane];
-        cs = misc[20 + lane];
-        if (!RING) {
-            if (a.out_mean) a.out_mean[(int64_t)seg * NMFCC + lane] = cm;
-            if (a.out_std) a.out_std[(int64_t)seg * NMFCC + lane] = cs;
+        lds_order();
+        if (lane < NMFCC && !RING) {
+            if (a.out_mean) a.out_mean[(int64_t)seg * NMFCC + lane] = misc[lane];
+            if (a.out_std) a.out_std[(int64_t)seg * NMFCC + lane] = misc[20 + lane];
         }
-    }
-    if (!a.has_template) continue;
-    if (lane == 0) {
-        float c32[2 * NMFCC];
-        double c64[2 * NMFCC];
-        for (int i = 0; i < 2 * NMFCC; ++i) { c32[i] = misc[i]; c64[i] = (double)misc[i]; }
-        const double score = a.cand_f32 ? score_f32cand(a.tmpl, a.tmpl + NMFCC, c32, c32 + NMFCC)
-                                        : score_f64cand(a.tmpl, a.tmpl + NMFCC, c64, c64 + NMFCC);
-        const int match = score >= a.threshold;
-        // fp64 re-score: decisions within the margin of the threshold, and very
-        // short segments (T <= kRescoreFrames) whose 2..16-frame std vectors are
-        // too ill-conditioned for the float32 pipeline to meet 1e-4.
-        const bool near = fabs(score - a.threshold) < a.rescore_margin || (1 + v.len / HOP) <= kRescoreFrames;
-        if (RING) {
-            a.events[seg].score = score;
-            a.events[seg].match = match;
-        } else {
-            a.out_score[seg] = score;
-            if (a.out_match) a.out_match[seg] = (uint8_t)match;
+        if (a.has_template) {
+            // wave-parallel dots (fixed butterfly order), lane 0 finishes the score
+            const bool act = lane < NMFCC;
+            const float cmf = act ? misc[lane] : 0.0f, csf = act ? misc[20 + lane] : 0.0f;
+            const float tmf = act ? a.tmpl[lane] : 0.0f, tsf = act ? a.tmpl[NMFCC + lane] : 0.0f;
+            double score;
+            if (a.cand_f32) {   // float32 candidates: float products, float-rounded dots (sdot)
+                const float uv_m = (float)wave_sum_d((double)(tmf * cmf)), vv_m = (float)wave_sum_d((double)(cmf * cmf));
+                const float uv_s = (float)wave_sum_d((double)(tsf * csf)), vv_s = (float)wave_sum_d((double)(csf * csf));
+                score = score_f32_finish(a.uu_m32, a.uu_s32, uv_m, vv_m, uv_s, vv_s);
+            } else {
+                const double uv_m = wave_sum_d((double)tmf * (double)cmf), vv_m = wave_sum_d((double)cmf * (double)cmf);
+                const double uv_s = wave_sum_d((double)tsf * (double)csf), vv_s = wave_sum_d((double)csf * (double)csf);
+                score = score_f64_finish((double)a.uu_m32, (double)a.uu_s32, uv_m, vv_m, uv_s, vv_s);
+            }
+            if (lane == 0) {
+            const int match = score >= a.threshold;
+            // fp64 re-score: decisions within the margin of the threshold, and very
+            // short segments (T <= kRescoreFrames) whose 2..16-frame std vectors are
+            // too ill-conditioned for the float32 pipeline to meet 1e-4.
+            const bool near = fabs(score - a.threshold) < a.rescore_margin || (1 + v.len / HOP) <= kRescoreFrames;
+            if (RING) {
+                a.events[seg].score = score;
+                a.events[seg].match = match;
+            } else {
+                a.out_score[seg] = score;
+                if (a.out_match) a.out_match[seg] = (uint8_t)match;
+            }
+            if (near && a.rescore_list) {
+                const int slot = atomicAdd(a.rescore_count, 1);
+                if (slot < a.rescore_cap) a.rescore_list[slot] = seg;
+            }
+            }
         }
-        if (near && a.rescore_list) {
-            const int slot = atomicAdd(a.rescore_count, 1);
-            if (slot < a.rescore_cap) a.rescore_list[slot] = seg;
-        }
-    }
-    lds_order();
+        lds_order();
     }   // work loop
 }
 
@@ -473,9 +649,13 @@ hipError_t launch_advance_watermark(int32_t* ev_base, const int32_t* n_events, h
     return hipGetLastError();
 }
 
+int score_grid(int n_seg, int ring_mode) {
+    return ring_mode ? kScoreGridRing : max(1, min((n_seg + WAVES - 1) / WAVES, kScoreGridMax));
+}
+
 hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mode, hipStream_t s) {
     if (a.n_seg <= 0) return hipSuccess;
-    const int grid = ring_mode ? 256 : min((a.n_seg + WAVES - 1) / WAVES, kScoreGridMax);
+    const int grid = score_grid(a.n_seg, ring_mode);
     hipError_t e = hipMemsetAsync(a.work, 0, sizeof(int32_t), s);
     if (e != hipSuccess) return e;
     if (ring_mode)

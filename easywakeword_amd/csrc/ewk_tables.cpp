@@ -97,7 +97,11 @@ void build_tables(Tables* t) {
     }
     std::vector<float> mel(NMEL * NBIN);
     mel_dense(mel.data());
-    int off = 0;
+    static const int kGroupW[8] = {2, 2, 2, 3, 4, 6, 9, 12};   // == kMelW in ewk_mfcc.hip
+    int it0[8];
+    int acc = 0;
+    for (int i = 0; i < 8; ++i) { it0[i] = acc; acc += kGroupW[i]; }
+    t->ok = acc == MEL_ITERS;
     for (int m = 0; m < NMEL; ++m) {
         int lo = -1, hi = -1;
         for (int k = 0; k < NBIN; ++k)
@@ -107,13 +111,12 @@ void build_tables(Tables* t) {
             }
         if (lo < 0) { lo = 0; hi = -1; }
         const int n = hi - lo + 1;
+        const int i = m / 16, j = m % 16;
+        if (n > kGroupW[i] || lo + kGroupW[i] > SCR_FRAME) t->ok = 0;
         t->band_lo[m] = lo;
-        t->band_n[m] = n;
-        t->band_off[m] = off;
-        for (int q = 0; q < n && off + q < MELW_CAP; ++q) t->melw[off + q] = 0.25f * mel[m * NBIN + lo + q];
-        off += n;
+        for (int q = 0; q < kGroupW[i]; ++q)
+            t->wpad[(it0[i] + q) * 16 + j] = q < n ? 0.25f * mel[m * NBIN + lo + q] : 0.0f;
     }
-    t->melw_count = off;
     double d[NMFCC * NMEL];
     dct_rows(d);
     for (int i = 0; i < NMFCC * NMEL; ++i) t->dct[i] = (float)d[i];

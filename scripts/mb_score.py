@@ -1,0 +1,31 @@
+"""Scorer microbenchmark: time k_score_f32 over the bench's ragged batch distribution.
+Usage: python scripts/mb_score.py [n_segments] [reps]   (EWK_LIB selects the .so variant)"""
+import os, sys, time
+import numpy as np
+ROOT = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+import torch
+import bench
+import easywakeword_amd as ewa
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+dev = torch.device("cuda", 0)
+word = bench.load_word()
+pcm, off, ln, frames, lengths, offsets = bench.make_segments(torch, dev, n, 1234, word)
+mean = torch.empty((n, 20), device=dev); std = torch.empty((n, 20), device=dev)
+score = torch.empty(n, device=dev, dtype=torch.float64); match = torch.empty(n, device=dev, dtype=torch.uint8)
+e = ewa.Engine()
+e.template_from_pcm(word)
+s = torch.cuda.Stream(dev); torch.cuda.set_stream(s)
+def step():
+    e.score_device(pcm.data_ptr(), off.data_ptr(), ln.data_ptr(), n, mean.data_ptr(), std.data_ptr(),
+                   score.data_ptr(), match.data_ptr(), s.cuda_stream)
+step(); torch.cuda.synchronize()
+e.profile(True)
+for _ in range(reps): step()
+torch.cuda.synchronize()
+ms, k = e.profile_read(0)
+ms /= k
+lib = os.path.basename(os.environ.get("EWK_LIB", "libewk.so"))
+print(f"{lib:28s} {ms:8.3f} ms  {frames/ms/1e6:7.3f} Gframes/s  frac={frames*640/(ms/1e3)/8e12:.4f}  "
+      f"matches={int(match.sum())} nan={int(torch.isnan(score).sum())} s0={float(score[0]):.4f}")
