@@ -18,7 +18,6 @@ constexpr int NMEL = 128;
 constexpr int NMFCC = EWK_N_MFCC;    // 20
 constexpr int MEL_ITERS = 40;        // unrolled mel FMAs per lane: sum of per-group band widths
 constexpr int DCT_PITCH = 130;       // LDS row pitch of the DCT table (bank-conflict free A reads)
-constexpr int TILE_PITCH = 130;      // LDS row pitch of the per-wave log-mel tile
 constexpr int SCR_FRAME = 272;       // per-frame FFT scratch floats (16 rows x 17)
 constexpr int WAVES = 4;             // waves per workgroup in the fp32 scorer
 

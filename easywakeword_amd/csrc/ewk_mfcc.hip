@@ -47,23 +47,28 @@ namespace ewk {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-// LDS carve (bytes, every offset a multiple of 16).
-constexpr int L_WIN2 = 0;
-constexpr int L_TW1 = L_WIN2 + 256 * 8;
-constexpr int L_TW2 = L_TW1 + 256 * 8;
-constexpr int L_BLO = L_TW2 + 256 * 8;
-constexpr int L_WPAD = L_BLO + NMEL * 4;
-constexpr int L_DCT = L_WPAD + MEL_ITERS * 16 * 4;
+// LDS carve (bytes, every offset a multiple of 16).  The per-lane table rows are
+// transposed to [lane j][index] with a 144-B (36-dword) row pitch so one
+// ds_read_b128 fetches 2 float2 entries and a 16-lane group spans all 64 banks.
+constexpr int TP = 18;                                    // float2 pitch of a [j][16] table row
+constexpr int WP = 52;                                    // float pitch of the [j][48] mel weight row (13 chunks: b128/b64 conflict free)
+constexpr int L_WIN2 = 0;                                 // [j][n1] = win2[16*n1 + j]
+constexpr int L_TW1 = L_WIN2 + 16 * TP * 8;               // [j][k1-1] = tw1[16*k1 + j], k1 = 1..15
+constexpr int L_TW2 = L_TW1 + 16 * TP * 8;                // [j][k2] = tw2[j + 16*k2]
+constexpr int L_WPAD = L_TW2 + 16 * TP * 8;               // [j][kMelOff[i] + q] = wpad[16*(it0_i + q) + j]
+constexpr int L_BLO = L_WPAD + 16 * WP * 4;
+constexpr int L_DCT = L_BLO + NMEL * 4;
 constexpr int L_SHARED_END = ((L_DCT + NMFCC * DCT_PITCH * 4) + 15) & ~15;
 constexpr int W_SCR = 0;                                  // 4 frames x 272 floats (also the sample staging)
-constexpr int W_TILE = W_SCR + 4 * SCR_FRAME * 4;         // 16 x 130 floats
-constexpr int W_MISC = W_TILE + 16 * TILE_PITCH * 4;      // 64 floats
-constexpr int W_BYTES = ((W_MISC + 64 * 4) + 15) & ~15;
+constexpr int W_TILE = W_SCR + 4 * SCR_FRAME * 4;         // 16 x 128 floats, XOR-swizzled rows
+constexpr int W_MISC = W_SCR;                             // 64 floats, aliases the FFT scratch (epilogue only)
+constexpr int W_BYTES = W_TILE + 16 * NMEL * 4;
 constexpr int LDS_BYTES = L_SHARED_END + WAVES * W_BYTES;
 constexpr int kRescoreFrames = 16;
 constexpr int kStage = 1024;                              // staged samples per pass (>= 3*160 + 512)
 static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU must fit");
 static_assert(kStage <= 4 * SCR_FRAME, "staging must fit the FFT scratch");
+
 
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 
@@ -104,34 +109,59 @@ __device__ __forceinline__ void dft16_perm(float2 (&x)[16]) {
 // Natural-order accessor of dft16_perm's output: X[k] lives in slot perm(k).
 __device__ __forceinline__ constexpr int dperm(int k) { return 4 * (k & 3) + (k >> 2); }
 
-struct SegView {
-    const float* p;   // linear: segment base; ring: stream ring base
-    int64_t start;    // ring: physical index of sample 0
-    int64_t ring;     // 0 = linear
+// Log-mel tile: 16 frame rows x 128 bands, row r holds band m at column m ^ swz(r).
+// swz(r) takes 16 distinct even values for r = 0..15 and flips bit 4 between rows
+// 2p and 2p+1, so the mel stage's row-pair writes (ds_write_b32, 32-bank halves)
+// and the MFMA B-operand reads (16 rows x 2 k-lanes per half) are both
+// bank-conflict free; the parking copy moves the tile as a flat array.
+__device__ __forceinline__ int tile_swz(int r) { return (r & 14) | ((r & 1) << 4); }
+
+// Segment samples through a buffer descriptor: the hardware range check returns 0
+// outside [0, len) (negative offsets wrap to huge unsigned ones), which is exactly
+// stft(center=True, pad_mode='constant').  Ring segments wrap at the stream ring.
+template <int RING>
+struct SegSrc {
+    __amdgpu_buffer_rsrc_t rsrc;   // linear: the segment; ring: the whole stream ring
     int32_t len;
+    int32_t wrap_at;               // ring: q >= wrap_at -> physical q + start - ring
+    int32_t start;                 // ring: physical index of sample 0
+    int32_t ring;
 };
 
-__device__ __forceinline__ float seg_sample(const SegView& v, int q) {
-    if (q < 0 || q >= v.len) return 0.0f;
-    int64_t idx = v.start + q;
-    if (v.ring && idx >= v.ring) idx -= v.ring;
-    return v.p[idx];
+template <int RING>
+__device__ __forceinline__ SegSrc<RING> make_src(const float* p, int64_t start, int64_t ring, int32_t len) {
+    SegSrc<RING> v;
+    const float* b = RING ? p : p + start;
+    const uint64_t bu = (uint64_t)b;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)bu);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(bu >> 32));
+    const float* bb = (const float*)(((uint64_t)hi << 32) | lo);
+    const int32_t n = __builtin_amdgcn_readfirstlane(RING ? (int32_t)ring : len);
+    v.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)bb, (short)0, n * 4, 0x00020000);
+    v.len = __builtin_amdgcn_readfirstlane(len);
+    v.start = __builtin_amdgcn_readfirstlane((int32_t)start);
+    v.ring = __builtin_amdgcn_readfirstlane((int32_t)ring);
+    v.wrap_at = v.ring - v.start;
+    return v;
 }
 
 // Coalesced staging loads: lane l fetches samples q0 + 64*c + l, c = 0..15.
-__device__ __forceinline__ void stage_load(const SegView& v, int q0, int lane, float (&r)[16]) {
-    const float* base = v.p + v.start;            // linear: segment start; ring: wraps below
-    const int ring = (int)v.ring;
-    const int wrap_at = ring ? ring - (int)v.start : 0x7fffffff;   // q >= wrap_at -> q - ring
+template <int RING>
+__device__ __forceinline__ void stage_load(const SegSrc<RING>& v, int q0, int lane, float (&r)[16]) {
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
         const int q = q0 + 64 * c + lane;
-        const bool in = (unsigned)q < (unsigned)v.len;
 #if EWK_ABLATE & 1
-        r[c] = in ? (float)((q * 7) & 255) * 1e-3f : 0.0f;
+        r[c] = ((unsigned)q < (unsigned)v.len) ? (float)((q * 7) & 255) * 1e-3f : 0.0f;
 #else
-        const int off = q >= wrap_at ? q - ring : q;
-        r[c] = in ? base[off] : 0.0f;
+        int off;
+        if (RING) {
+            const int phys = q >= v.wrap_at ? q - v.wrap_at : q + v.start;
+            off = (unsigned)q < (unsigned)v.len ? phys * 4 : -1;
+        } else {
+            off = q * 4;
+        }
+        r[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(v.rsrc, off, 0, 0));
 #endif
     }
 }
@@ -142,34 +172,50 @@ __device__ __forceinline__ void stage_store(float* stage, int lane, const float 
 }
 
 constexpr int kMelW[8] = {2, 2, 2, 3, 4, 6, 9, 12};   // per 16-band group (checked on the host)
+constexpr int kMelIt0[8] = {0, 2, 4, 6, 9, 13, 19, 28};    // first weight of group i in Tables::wpad
+// Each group's weights start on a b64 (widths 2) or b128 boundary of the LDS row so one
+// group is fetched with 1-3 wide reads right before it is used.
+constexpr int kMelOff[8] = {0, 2, 4, 8, 12, 16, 24, 36};
+constexpr int kMelRow = 48;
+static_assert(kMelRow <= WP && WP % 4 == 0, "mel weight rows");
 
 // One 4-frame pass: frames t0 + (lane>>4), samples already staged in `scr`.
 // Writes rows [row0, row0+4) of the log-mel tile (invalid frames -> 0) and
 // returns the per-lane max/min of the valid log-mel values.  If `next` is
 // set, the next pass's samples are fetched meanwhile and staged at the end.
-__device__ __forceinline__ void frame_pass(const SegView& v, int t0, int T, int row0, bool next,
+// `lo[i]` = first bin of band j + 16 i (per lane, loaded once per kernel).
+template <int RING>
+__device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T, int row0, bool next,
                                            const unsigned char* smem, float* scr, float* tile,
-                                           int lane, float& vmax, float& vmin) {
-    const float2* s_win2 = reinterpret_cast<const float2*>(smem + L_WIN2);
-    const float2* s_tw1 = reinterpret_cast<const float2*>(smem + L_TW1);
-    const float2* s_tw2 = reinterpret_cast<const float2*>(smem + L_TW2);
-    const int* s_blo = reinterpret_cast<const int*>(smem + L_BLO);
-    const float* s_wpad = reinterpret_cast<const float*>(smem + L_WPAD);
-
+                                           int lane, const int (&lo)[8], float& vmax, float& vmin) {
     const int f = lane >> 4, j = lane & 15;
     const int t = t0 + f;
     const bool valid = t < T;
     float* sc = scr + f * SCR_FRAME;
 
     // ---- window the staged samples: lane j holds z[16*n1 + j] = x[32*n1+2j] + i x[32*n1+2j+1]
+    // (16 single ds_read_b64: the compiler would pair them into ds_read2_b64, which
+    // costs the LDS twice the cycles per byte)
     float2 a[16];
     {
-        const float2* st2 = reinterpret_cast<const float2*>(scr + f * HOP + 2 * j);
+        const uint32_t sa = (uint32_t)(uintptr_t)(scr + f * HOP + 2 * j);
+        float2 x[16];
+#define EWK_LD64(n) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(x[n]) : "v"(sa), "i"(128 * (n)) : "memory")
+        EWK_LD64(0); EWK_LD64(1); EWK_LD64(2); EWK_LD64(3); EWK_LD64(4); EWK_LD64(5); EWK_LD64(6); EWK_LD64(7);
+        EWK_LD64(8); EWK_LD64(9); EWK_LD64(10); EWK_LD64(11); EWK_LD64(12); EWK_LD64(13); EWK_LD64(14); EWK_LD64(15);
+#undef EWK_LD64
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
+                       "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]),
+                       "+v"(x[15])
+                     :
+                     : "memory");
+        const float4* w4 = reinterpret_cast<const float4*>(smem + L_WIN2) + j * (TP / 2);
 #pragma unroll
-        for (int n1 = 0; n1 < 16; ++n1) {
-            const float2 x = st2[16 * n1];
-            const float2 w = s_win2[16 * n1 + j];
-            a[n1] = make_float2(x.x * w.x, x.y * w.y);
+        for (int c = 0; c < 8; ++c) {
+            const float4 w = w4[c];
+            a[2 * c] = make_float2(x[2 * c].x * w.x, x[2 * c].y * w.y);
+            a[2 * c + 1] = make_float2(x[2 * c + 1].x * w.z, x[2 * c + 1].y * w.w);
         }
     }
     lds_order();
@@ -178,97 +224,128 @@ __device__ __forceinline__ void frame_pass(const SegView& v, int t0, int T, int 
     if (next) stage_load(v, (t0 + 4) * HOP - NFFT / 2, lane, pf);
     // ---- DFT16 over n1, twiddle W256^(j*k1)
     dft16_perm(a);
+    {
+        const float4* t4 = reinterpret_cast<const float4*>(smem + L_TW1) + j * (TP / 2);
 #pragma unroll
-    for (int k1 = 1; k1 < 16; ++k1) a[dperm(k1)] = cmul(a[dperm(k1)], s_tw1[k1 * 16 + j]);
-    // ---- transpose through LDS (real, then imaginary half): lane k1 <- A_{n2}[k1]
+        for (int c = 0; c < 8; ++c) {
+            const float4 w = t4[c];   // k1 = 2c+1, 2c+2
+            a[dperm(2 * c + 1)] = cmul(a[dperm(2 * c + 1)], make_float2(w.x, w.y));
+            if (c < 7) a[dperm(2 * c + 2)] = cmul(a[dperm(2 * c + 2)], make_float2(w.z, w.w));
+        }
+    }
+    // ---- transpose through LDS (real, then imaginary half): lane k1 <- A_{n2}[k1].
+    // Row r (16 floats) keeps column n in 4-float chunk (n>>2) ^ ((r>>2)&3): the
+    // column writes (ds_write_b32, frames f/f+1 272 floats apart) and the row reads
+    // (ds_read_b128) are both bank-conflict free.
     float2 b[16];
 #if EWK_ABLATE & 2
 #pragma unroll
     for (int k1 = 0; k1 < 16; ++k1) b[k1] = a[dperm(k1)];
 #else
+    {
+        const int jc = 4 * (j >> 2), jl = j & 3;
+        const float4* rd = reinterpret_cast<const float4*>(sc + 16 * j);
+        const int rsw = (j >> 2) & 3;
 #pragma unroll
-    for (int k1 = 0; k1 < 16; ++k1) sc[k1 * 17 + j] = a[dperm(k1)].x;
-    lds_order();
+        for (int half = 0; half < 2; ++half) {
 #pragma unroll
-    for (int n2 = 0; n2 < 16; ++n2) b[n2].x = sc[j * 17 + n2];
-    lds_order();
+            for (int k1 = 0; k1 < 16; ++k1) {
+                const float2 v = a[dperm(k1)];
+                sc[16 * k1 + (jc ^ (4 * ((k1 >> 2) & 3))) + jl] = half ? v.y : v.x;
+            }
+            lds_order();
 #pragma unroll
-    for (int k1 = 0; k1 < 16; ++k1) sc[k1 * 17 + j] = a[dperm(k1)].y;
-    lds_order();
-#pragma unroll
-    for (int n2 = 0; n2 < 16; ++n2) b[n2].y = sc[j * 17 + n2];
-    lds_order();
+            for (int c = 0; c < 4; ++c) {
+                const float4 r = rd[c ^ rsw];
+                if (half) { b[4 * c].y = r.x; b[4 * c + 1].y = r.y; b[4 * c + 2].y = r.z; b[4 * c + 3].y = r.w; }
+                else      { b[4 * c].x = r.x; b[4 * c + 1].x = r.y; b[4 * c + 2].x = r.z; b[4 * c + 3].x = r.w; }
+            }
+            lds_order();
+        }
+    }
 #endif
     // ---- DFT16 over n2: Z[j + 16*k2] = b[dperm(k2)]
     dft16_perm(b);
-    // ---- untangle: partner Z[(256-k) & 255], k = j + 16*k2
-    float2 zp[16];
-#if EWK_ABLATE & 2
+    // ---- untangle + power, one bin column at a time.  Partner Z[(256-k) & 255] of
+    // k = j + 16*k2 comes straight from the partner lane's registers: for j >= 1 it is
+    // lane 16-j's slot 15-k2 (DPP row_mirror then row_shr:1); lane 0 keeps its own
+    // slot (16-k2)&15.  P'[k] = |2 X[k]|^2 = |A - i W512^k B|^2 with
+    // A = Z[k] + conj(Zp), B = Z[k] - conj(Zp).
+    {
+        const float4* c4 = reinterpret_cast<const float4*>(smem + L_TW2) + j * (TP / 2);
 #pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) zp[k2] = b[dperm(15 - k2)];
-#else
+        for (int c = 0; c < 8; ++c) {
+            const float4 w = c4[c];
 #pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) sc[j + 16 * k2] = b[dperm(k2)].x;
-    lds_order();
-#pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) zp[k2].x = sc[(256 - (j + 16 * k2)) & 255];
-    lds_order();
-#pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) sc[j + 16 * k2] = b[dperm(k2)].y;
-    lds_order();
-#pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) zp[k2].y = sc[(256 - (j + 16 * k2)) & 255];
-    lds_order();
-#endif
-    // P'[k] = |2 X[k]|^2 = |A - i W512^k B|^2, A = Z[k] + conj(Zp), B = Z[k] - conj(Zp)
-    float pw[16];
-#pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) {
-        const float2 z = b[dperm(k2)], p = zp[k2];
-        const float ar = z.x + p.x, ai = z.y - p.y;
-        const float br = z.x - p.x, bi = z.y + p.y;
-        const float2 cs = s_tw2[j + 16 * k2];
-        const float yr = ar - cs.y * br + cs.x * bi;
-        const float yi = ai - cs.y * bi - cs.x * br;
-        pw[k2] = yr * yr + yi * yi;
+            for (int u = 0; u < 2; ++u) {
+                const int k2 = 2 * c + u;
+                const float2 src = b[dperm(15 - k2)], own = b[dperm((16 - k2) & 15)];
+                const int mx = __builtin_amdgcn_mov_dpp(__float_as_int(src.x), 0x140, 0xf, 0xf, false);   // row_mirror
+                const int my = __builtin_amdgcn_mov_dpp(__float_as_int(src.y), 0x140, 0xf, 0xf, false);
+                const float px = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.x), mx, 0x111, 0xf, 0xf, false));
+                const float py = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.y), my, 0x111, 0xf, 0xf, false));
+                const float2 cs = u ? make_float2(w.z, w.w) : make_float2(w.x, w.y);
+                const float2 z = b[dperm(k2)];
+                const float ar = z.x + px, ai = z.y - py;
+                const float br = z.x - px, bi = z.y + py;
+                const float yr = ar - cs.y * br + cs.x * bi;
+                const float yi = ai - cs.y * bi - cs.x * br;
+                sc[j + 16 * k2] = yr * yr + yi * yi;
+            }
+        }
     }
-    float p256 = 0.0f;
-    if (j == 0) {   // X[256] = Re Z[0] - Im Z[0]
+    {   // bin 256 (X[256] = Re Z[0] - Im Z[0]) and the zero pad the unrolled band loops read past it
         const float2 z0 = b[dperm(0)];
         const float y = 2.0f * (z0.x - z0.y);
-        p256 = y * y;
+        sc[256 + j] = (j == 0) ? y * y : 0.0f;
     }
-#pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) sc[j + 16 * k2] = pw[k2];
-    // bin 256 and the zero pad the unrolled band loops read past it
-    sc[256 + j] = (j == 0) ? p256 : 0.0f;
     lds_order();
     // ---- mel + log: lane j computes bands m = j + 16*i of its frame
-    float* trow = tile + (row0 + f) * TILE_PITCH;
-    int it = 0;
+    float db[8];
+    {
+        const float* wrow = reinterpret_cast<const float*>(smem + L_WPAD) + j * WP;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int m = j + 16 * i;
-        const int lo = s_blo[m];
-        float acc = 0.0f;
+        for (int i = 0; i < 8; ++i) {
+            float wv[12];
+            if (kMelW[i] <= 2) {
+                const float2 w = *reinterpret_cast<const float2*>(wrow + kMelOff[i]);
+                wv[0] = w.x; wv[1] = w.y;
+            } else {
+#pragma unroll
+                for (int c = 0; c < (kMelW[i] + 3) / 4; ++c) {
+                    const float4 w = *reinterpret_cast<const float4*>(wrow + kMelOff[i] + 4 * c);
+                    wv[4 * c] = w.x; wv[4 * c + 1] = w.y; wv[4 * c + 2] = w.z; wv[4 * c + 3] = w.w;
+                }
+            }
+            const float* sp = sc + lo[i];
+            float acc = 0.0f;
 #if EWK_ABLATE & 4
-        acc = s_wpad[it * 16 + j] * sc[lo] + 1.0f;
+            acc = wv[0] * sp[0] + 1.0f;
 #else
 #pragma unroll
-        for (int q = 0; q < kMelW[i]; ++q) acc = fmaf(s_wpad[(it + q) * 16 + j], sc[lo + q], acc);
+            for (int q = 0; q < kMelW[i]; ++q) acc = fmaf(wv[q], sp[q], acc);
 #endif
-        it += kMelW[i];
 #if EWK_ABLATE & 8
-        float db = acc;
+            db[i] = acc;
 #else
-        // 10*log10(x) = (10*log10(2)) * log2(x), v_log_f32
-        float db = 3.0102999566398120f * __log2f(fmaxf(1e-10f, acc));
+            // 10*log10(x) = (10*log10(2)) * log2(x), v_log_f32
+            db[i] = 3.0102999566398120f * __log2f(fmaxf(1e-10f, acc));
 #endif
-        if (valid) {
-            vmax = fmaxf(vmax, db);
-            vmin = fminf(vmin, db);
         }
-        trow[m] = valid ? db : 0.0f;
+    }
+    lds_order();
+    {
+        const int r = row0 + f;
+        const int sw = tile_swz(r);
+        const int jx = j ^ (sw & 15), sb = sw >> 4;
+        float* re = tile + r * NMEL + jx + 16 * sb;   // even i: column 16*(i+sb) + jx
+        float* ro = tile + r * NMEL + jx - 16 * sb;   // odd  i: column 16*(i-sb) + jx
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            vmax = fmaxf(vmax, valid ? db[i] : -INFINITY);
+            vmin = fminf(vmin, valid ? db[i] : INFINITY);
+            ((i & 1) ? ro : re)[16 * i] = valid ? db[i] : 0.0f;
+        }
     }
     lds_order();
     if (next) stage_store(scr, lane, pf);
@@ -281,22 +358,35 @@ __device__ __forceinline__ void tile_dct_stats(const float* tile, const float* s
                                                int lane, float (&cref)[8], double (&s1)[8], double (&s2)[8]) {
     const int col = lane & 15, h = lane >> 4;
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    const float* brow = tile + col * TILE_PITCH + h;
+    // B[k = 4s + h][col] = tile row col, band 4s + h, stored at column (4s + h) ^ swz(col);
+    // swz < 32, so bands 32u + b sit at 32u + (b ^ swz): 8 per-lane offsets + immediates.
+    const int sw = tile_swz(col);
+    int boff[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) boff[s] = col * NMEL + ((4 * s + h) ^ sw);
     const float* arow0 = s_dct + col * DCT_PITCH + h;
     const float* arow1 = s_dct + (16 + (col & 3)) * DCT_PITCH + h;
     const bool a1ok = col < 4;
-#pragma unroll 8
-    for (int s = 0; s < 32; ++s) {
-        const float bv = brow[4 * s];
-        const float a0 = arow0[4 * s];
-        const float a1 = a1ok ? arow1[4 * s] : 0.0f;
+#pragma unroll
+    for (int s0 = 0; s0 < 32; s0 += 8) {   // operands of 8 k-steps in flight, then 16 MFMAs
+        float bv[8], av0[8], av1[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            bv[u] = tile[boff[u] + 32 * (s0 >> 3)];
+            av0[u] = arow0[4 * (s0 + u)];
+            const float x1 = arow1[4 * (s0 + u)];
+            av1[u] = a1ok ? x1 : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
 #if EWK_ABLATE & 16
-        acc0[s & 3] += a0 * bv;
-        acc1[s & 3] += a1 * bv;
+            acc0[u & 3] += av0[u] * bv[u];
+            acc1[u & 3] += av1[u] * bv[u];
 #else
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, bv, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, bv, acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[u], bv[u], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[u], bv[u], acc1, 0, 0, 0);
 #endif
+        }
     }
     lds_order();
     float c[8] = {acc0[0], acc0[1], acc0[2], acc0[3], acc1[0], acc1[1], acc1[2], acc1[3]};
@@ -332,10 +422,16 @@ __device__ __forceinline__ void finish_stats(int T, const float (&cref)[8], doub
     }
 }
 
-// Whole segment for one wave.  gscr: this wave's log-mel scratch ([tile][16][64] float2),
-// able to hold `scr_tiles` tiles.
-__device__ void segment_stats(const SegView& v, const unsigned char* smem, float* scr, float* tile,
-                              float2* gscr, int scr_tiles, int lane, double (&s1)[8], double (&s2)[8]) {
+__device__ __forceinline__ void zero_row(float* tile, int r, int lane) {
+    for (int m = lane & 15; m < NMEL; m += 16) tile[r * NMEL + m] = 0.0f;
+}
+
+// Whole segment for one wave.  gscr: this wave's log-mel scratch (flat 16x128-float
+// tiles, float4 [tile][8][64]), able to hold `scr_tiles` tiles.
+template <int RING>
+__device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, float* scr, float* tile,
+                              float4* gscr, int scr_tiles, int lane, const int (&lo)[8], double (&s1)[8],
+                              double (&s2)[8]) {
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     const int T = 1 + v.len / HOP;
     const int ntile = (T + 15) >> 4;
@@ -351,24 +447,21 @@ __device__ void segment_stats(const SegView& v, const unsigned char* smem, float
         stage_store(scr, lane, r);
         lds_order();
     }
-    // tile copy mapping: lane l owns row l>>2, columns (l&3)*32 .. +32 as 16 float2
-    const int crow = lane >> 2, ccol = (lane & 3) * 32;
+    float4* tile4 = reinterpret_cast<float4*>(tile);
     for (int tile_i = 0; tile_i < ntile; ++tile_i) {
 #pragma unroll 1
         for (int p = 0; p < 4; ++p) {
             const int pass = tile_i * 4 + p;
             if (pass < npass)
-                frame_pass(v, pass * 4, T, p * 4, pass + 1 < npass, smem, scr, tile, lane, vmax, vmin);
-            else {   // rows of frames past T: zero (ignored by the statistics)
-                for (int m = lane & 15; m < NMEL; m += 16) tile[(p * 4 + (lane >> 4)) * TILE_PITCH + m] = 0.0f;
-            }
+                frame_pass(v, pass * 4, T, p * 4, pass + 1 < npass, smem, scr, tile, lane, lo, vmax, vmin);
+            else   // rows of frames past T: zero (ignored by the statistics)
+                zero_row(tile, p * 4 + (lane >> 4), lane);
         }
         lds_order();
         if (park) {
-            const float2* src = reinterpret_cast<const float2*>(tile + crow * TILE_PITCH + ccol);
-            float2* dst = gscr + (int64_t)tile_i * 16 * 64 + lane;
+            float4* dst = gscr + (int64_t)tile_i * 8 * 64 + lane;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) dst[k * 64] = src[k];
+            for (int k = 0; k < 8; ++k) dst[k * 64] = tile4[k * 64 + lane];
         }
         tile_dct_stats(tile, s_dct, tile_i, T, lane, cref, s1, s2);
     }
@@ -385,18 +478,19 @@ __device__ void segment_stats(const SegView& v, const unsigned char* smem, float
 #pragma unroll
         for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; }
         if (park) {
-            float2 nx[16];
+            float4 nx[8];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) nx[k] = gscr[k * 64 + lane];
+            for (int k = 0; k < 8; ++k) nx[k] = gscr[k * 64 + lane];
             for (int tile_i = 0; tile_i < ntile; ++tile_i) {
-                float2* dst = reinterpret_cast<float2*>(tile + crow * TILE_PITCH + ccol);
 #pragma unroll
-                for (int k = 0; k < 16; ++k) dst[k] = make_float2(fmaxf(nx[k].x, theta), fmaxf(nx[k].y, theta));
+                for (int k = 0; k < 8; ++k)
+                    tile4[k * 64 + lane] = make_float4(fmaxf(nx[k].x, theta), fmaxf(nx[k].y, theta),
+                                                       fmaxf(nx[k].z, theta), fmaxf(nx[k].w, theta));
                 lds_order();
                 if (tile_i + 1 < ntile) {   // next tile's loads overlap this tile's MFMAs
-                    const float2* src = gscr + (int64_t)(tile_i + 1) * 16 * 64 + lane;
+                    const float4* src = gscr + (int64_t)(tile_i + 1) * 8 * 64 + lane;
 #pragma unroll
-                    for (int k = 0; k < 16; ++k) nx[k] = src[k * 64];
+                    for (int k = 0; k < 8; ++k) nx[k] = src[k * 64];
                 }
                 tile_dct_stats(tile, s_dct, tile_i, T, lane, cref, s1, s2);
             }
@@ -414,14 +508,17 @@ __device__ void segment_stats(const SegView& v, const unsigned char* smem, float
                 for (int p = 0; p < 4; ++p) {
                     const int pass = tile_i * 4 + p;
                     if (pass < npass)
-                        frame_pass(v, pass * 4, T, p * 4, pass + 1 < npass, smem, scr, tile, lane, d0, d1);
+                        frame_pass(v, pass * 4, T, p * 4, pass + 1 < npass, smem, scr, tile, lane, lo, d0, d1);
                     else
-                        for (int m = lane & 15; m < NMEL; m += 16) tile[(p * 4 + (lane >> 4)) * TILE_PITCH + m] = 0.0f;
+                        zero_row(tile, p * 4 + (lane >> 4), lane);
                 }
                 lds_order();
-                float* trow = tile + crow * TILE_PITCH + ccol;
 #pragma unroll
-                for (int k = 0; k < 32; ++k) trow[k] = fmaxf(trow[k], theta);
+                for (int k = 0; k < 8; ++k) {
+                    const float4 x = tile4[k * 64 + lane];
+                    tile4[k * 64 + lane] = make_float4(fmaxf(x.x, theta), fmaxf(x.y, theta),
+                                                       fmaxf(x.z, theta), fmaxf(x.w, theta));
+                }
                 lds_order();
                 tile_dct_stats(tile, s_dct, tile_i, T, lane, cref, s1, s2);
             }
@@ -534,16 +631,28 @@ __device__ __forceinline__ double score_f32_finish(float uu_m, float uu_s, float
 template <int RING>
 __global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__ tab, ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    // ---- cooperative table load (global -> LDS)
+    // ---- cooperative table load (global -> LDS), per-lane rows transposed
     {
-        const float4* g = reinterpret_cast<const float4*>(tab);
-        float4* s = reinterpret_cast<float4*>(smem);
-        // win2, tw1, tw2 are contiguous at the start of Tables (3 * 2048 B)
-        for (int i = threadIdx.x; i < 3 * 2048 / 16; i += blockDim.x) s[i] = g[i];
+        float2* sw2 = reinterpret_cast<float2*>(smem + L_WIN2);
+        float2* st1 = reinterpret_cast<float2*>(smem + L_TW1);
+        float2* st2 = reinterpret_cast<float2*>(smem + L_TW2);
+        for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+            const int j = i & 15, n = i >> 4;   // win2[16n + j], tw1[16n + j], tw2[j + 16n]
+            sw2[j * TP + n] = tab->win2[i];
+            if (n > 0) st1[j * TP + n - 1] = tab->tw1[i];
+            st2[j * TP + n] = tab->tw2[i];
+        }
         int* sb = reinterpret_cast<int*>(smem + L_BLO);
         for (int i = threadIdx.x; i < NMEL; i += blockDim.x) sb[i] = tab->band_lo[i];
         float* sw = reinterpret_cast<float*>(smem + L_WPAD);
-        for (int i = threadIdx.x; i < MEL_ITERS * 16; i += blockDim.x) sw[i] = tab->wpad[i];
+        for (int i = threadIdx.x; i < 16 * WP; i += blockDim.x) {
+            const int j = i / WP, o = i % WP;
+            float w = 0.0f;
+#pragma unroll
+            for (int g = 0; g < 8; ++g)
+                if (o >= kMelOff[g] && o < kMelOff[g] + kMelW[g]) w = tab->wpad[(kMelIt0[g] + o - kMelOff[g]) * 16 + j];
+            sw[i] = w;
+        }
         float* sd = reinterpret_cast<float*>(smem + L_DCT);
         for (int i = threadIdx.x; i < NMFCC * NMEL; i += blockDim.x)
             sd[(i / NMEL) * DCT_PITCH + (i % NMEL)] = tab->dct[i];
@@ -559,7 +668,13 @@ __global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__
     float* scr = reinterpret_cast<float*>(wbase + W_SCR);
     float* tile = reinterpret_cast<float*>(wbase + W_TILE);
     float* misc = reinterpret_cast<float*>(wbase + W_MISC);
-    float2* gscr = a.lm_scratch + (int64_t)(blockIdx.x * WAVES + wave) * a.lm_tiles * 16 * 64;
+    float4* gscr = reinterpret_cast<float4*>(a.lm_scratch) + (int64_t)(blockIdx.x * WAVES + wave) * a.lm_tiles * 8 * 64;
+    int lo[8];   // first bin of this lane's bands j + 16 i
+    {
+        const int* sb = reinterpret_cast<const int*>(smem + L_BLO);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) lo[i] = sb[(lane & 15) + 16 * i];
+    }
     // persistent waves pull segments from a work counter (ragged lengths balance)
     for (;;) {
         int idx = 0;
@@ -568,23 +683,25 @@ __global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__
         if (idx >= count) break;
         const int seg = base + idx;
 
-        SegView v;
+        int64_t start, ring = 0;
+        const float* p;
+        int32_t len;
         if (RING) {
             const ewk_event ev = a.events[seg];
-            v.p = a.pcm + (int64_t)ev.stream * a.ring_len;
-            v.start = ev.ring_start;
-            v.ring = a.ring_len;
-            v.len = ev.length;
             if (ev.flags & EWK_EV_SKIPPED) continue;
+            p = a.pcm + (int64_t)ev.stream * a.ring_len;
+            start = ev.ring_start;
+            ring = a.ring_len;
+            len = ev.length;
         } else {
-            v.p = a.pcm;
-            v.start = a.offsets[seg];
-            v.ring = 0;
-            v.len = a.lengths[seg];
+            p = a.pcm;
+            start = a.offsets[seg];
+            len = a.lengths[seg];
         }
+        const SegSrc<RING> v = make_src<RING>(p, start, ring, len);
 
         double st1[8], st2[8];
-        segment_stats(v, smem, scr, tile, gscr, a.lm_tiles, lane, st1, st2);
+        segment_stats(v, smem, scr, tile, gscr, a.lm_tiles, lane, lo, st1, st2);
 
         // ---- gather fp32-rounded mean/std into misc[0..19], misc[20..39]
         if ((lane & 15) == 0) {
@@ -673,6 +790,20 @@ hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mo
 // reference (wakeword.py:1105-1121 hands float64 ring slices to librosa).
 // ============================================================================
 // numpy's float64 pairwise add.reduce over n strided values (n <= 8192: one ufunc buffer)
+struct SegView {
+    const float* p;   // linear: segment base; ring: stream ring base
+    int64_t start;    // ring: physical index of sample 0
+    int64_t ring;     // 0 = linear
+    int32_t len;
+};
+
+__device__ __forceinline__ float seg_sample(const SegView& v, int q) {
+    if (q < 0 || q >= v.len) return 0.0f;
+    int64_t idx = v.start + q;
+    if (v.ring && idx >= v.ring) idx -= v.ring;
+    return v.p[idx];
+}
+
 __device__ double pw_sum(const double* a, int n, int stride) {
     if (n < 8) {
         double r = 0.0;
