@@ -75,7 +75,7 @@ struct ewk_engine {
     int32_t* d_work = nullptr;      // scorer work counter
     int32_t rescore_cap = 4096;
     DevBuf<double> f64_scratch;
-    DevBuf<float2> lm_scratch;      // parked log-mel tiles, kLmTiles x 8 KB per scorer wave
+    DevBuf<float2> lm_scratch;      // parked log-mel tiles + their DCT columns, kLmTiles x 10 KB per scorer wave
     int f64_grid = 64;
 
     // host-API staging
@@ -156,7 +156,7 @@ static hipError_t reserve_rescore(ewk_engine* e, int32_t n_seg) {
 // Size the per-wave log-mel scratch for a launch of `n_seg` segments.
 static hipError_t reserve_lm(ewk_engine* e, int32_t n_seg, int ring_mode) {
     const size_t waves = (size_t)score_grid(n_seg, ring_mode) * WAVES;
-    const size_t need = waves * kLmTiles * 16 * 64;
+    const size_t need = waves * kLmTiles * 20 * 64;   // float2 units: 8 KB tile + 2 KB DCT columns
     if (need <= e->lm_scratch.cap) return hipSuccess;
     hipError_t err = hipStreamSynchronize(e->stream);
     if (err != hipSuccess) return err;

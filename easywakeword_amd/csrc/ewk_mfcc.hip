@@ -43,7 +43,20 @@
 #define EWK_ABLATE 0   // timing-only ablations (scripts/mb_score.py); 0 in every real build
 #endif
 
+#ifndef EWK_TIMING
+#define EWK_TIMING 0   // per-phase s_memtime accounting (scripts/mb_score.py variants only)
+#endif
+
 namespace ewk {
+
+#if EWK_TIMING
+__device__ unsigned long long g_tim[24];
+#define EWK_TS(x) const uint64_t x = __builtin_amdgcn_s_memtime()
+#define EWK_TACC(i, a, b) (tim[i] += (b) - (a))
+#else
+#define EWK_TS(x)
+#define EWK_TACC(i, a, b)
+#endif
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
@@ -62,7 +75,8 @@ constexpr int L_SHARED_END = ((L_DCT + NMFCC * DCT_PITCH * 4) + 15) & ~15;
 constexpr int W_SCR = 0;                                  // 4 frames x 272 floats (also the sample staging)
 constexpr int W_TILE = W_SCR + 4 * SCR_FRAME * 4;         // 16 x 128 floats, XOR-swizzled rows
 constexpr int W_MISC = W_SCR;                             // 64 floats, aliases the FFT scratch (epilogue only)
-constexpr int W_BYTES = W_TILE + 16 * NMEL * 4;
+constexpr int W_TMIN = W_TILE + 16 * NMEL * 4;            // per-tile log-mel minima (kLmTiles floats)
+constexpr int W_BYTES = W_TMIN + ((kLmTiles * 4 + 15) & ~15);
 constexpr int LDS_BYTES = L_SHARED_END + WAVES * W_BYTES;
 constexpr int kRescoreFrames = 16;
 constexpr int kStage = 1024;                              // staged samples per pass (>= 3*160 + 512)
@@ -187,7 +201,9 @@ static_assert(kMelRow <= WP && WP % 4 == 0, "mel weight rows");
 template <int RING>
 __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T, int row0, bool next,
                                            const unsigned char* smem, float* scr, float* tile,
-                                           int lane, const int (&lo)[8], float& vmax, float& vmin) {
+                                           int lane, const int (&lo)[8], float& vmax, float& vmin,
+                                           uint64_t* tim = nullptr) {
+    EWK_TS(p0);
     const int f = lane >> 4, j = lane & 15;
     const int t = t0 + f;
     const bool valid = t < T;
@@ -219,9 +235,13 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
         }
     }
     lds_order();
+    EWK_TS(p1);
+    if (tim) EWK_TACC(8, p0, p1);
     // ---- prefetch the next pass while this one computes
     float pf[16];
     if (next) stage_load(v, (t0 + 4) * HOP - NFFT / 2, lane, pf);
+    EWK_TS(p2);
+    if (tim) EWK_TACC(9, p1, p2);
     // ---- DFT16 over n1, twiddle W256^(j*k1)
     dft16_perm(a);
     {
@@ -233,6 +253,8 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
             if (c < 7) a[dperm(2 * c + 2)] = cmul(a[dperm(2 * c + 2)], make_float2(w.z, w.w));
         }
     }
+    EWK_TS(p3);
+    if (tim) EWK_TACC(10, p2, p3);
     // ---- transpose through LDS (real, then imaginary half): lane k1 <- A_{n2}[k1].
     // Row r (16 floats) keeps column n in 4-float chunk (n>>2) ^ ((r>>2)&3): the
     // column writes (ds_write_b32, frames f/f+1 272 floats apart) and the row reads
@@ -264,8 +286,12 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
         }
     }
 #endif
+    EWK_TS(p4);
+    if (tim) EWK_TACC(11, p3, p4);
     // ---- DFT16 over n2: Z[j + 16*k2] = b[dperm(k2)]
     dft16_perm(b);
+    EWK_TS(p5);
+    if (tim) EWK_TACC(12, p4, p5);
     // ---- untangle + power, one bin column at a time.  Partner Z[(256-k) & 255] of
     // k = j + 16*k2 comes straight from the partner lane's registers: for j >= 1 it is
     // lane 16-j's slot 15-k2 (DPP row_mirror then row_shr:1); lane 0 keeps its own
@@ -300,6 +326,8 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
         sc[256 + j] = (j == 0) ? y * y : 0.0f;
     }
     lds_order();
+    EWK_TS(p6);
+    if (tim) EWK_TACC(13, p5, p6);
     // ---- mel + log: lane j computes bands m = j + 16*i of its frame
     float db[8];
     {
@@ -333,6 +361,8 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
 #endif
         }
     }
+    EWK_TS(p7);
+    if (tim) EWK_TACC(14, p6, p7);
     lds_order();
     {
         const int r = row0 + f;
@@ -348,14 +378,17 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
         }
     }
     lds_order();
+    EWK_TS(p8);
+    if (tim) EWK_TACC(15, p7, p8);
     if (next) stage_store(scr, lane, pf);
     lds_order();
+    EWK_TS(p9);
+    if (tim) EWK_TACC(16, p8, p9);
 }
 
-// DCT of one 16-frame log-mel tile on the matrix cores + fp64 statistics update.
-// Lane l holds C[row = 4h + r][frame col] of both row tiles (h = l>>4, col = l&15).
-__device__ __forceinline__ void tile_dct_stats(const float* tile, const float* s_dct, int tile_i, int T,
-                                               int lane, float (&cref)[8], double (&s1)[8], double (&s2)[8]) {
+// DCT of one 16-frame log-mel tile on the matrix cores.
+// Lane l gets C[row = 4h + r][frame col] of both row tiles (h = l>>4, col = l&15) in c[0..3], c[4..7].
+__device__ __forceinline__ void tile_dct(const float* tile, const float* s_dct, int lane, float (&c)[8]) {
     const int col = lane & 15, h = lane >> 4;
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     // B[k = 4s + h][col] = tile row col, band 4s + h, stored at column (4s + h) ^ swz(col);
@@ -389,12 +422,14 @@ __device__ __forceinline__ void tile_dct_stats(const float* tile, const float* s
         }
     }
     lds_order();
-    float c[8] = {acc0[0], acc0[1], acc0[2], acc0[3], acc1[0], acc1[1], acc1[2], acc1[3]};
-    if (tile_i == 0) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
-    }
-    if (tile_i * 16 + col < T) {
+    for (int i = 0; i < 4; ++i) { c[i] = acc0[i]; c[4 + i] = acc1[i]; }
+}
+
+// fp64 shifted sums of the frame columns that exist (d = c - cref).
+__device__ __forceinline__ void stats_add(const float (&c)[8], const float (&cref)[8], bool ok, double (&s1)[8],
+                                          double (&s2)[8]) {
+    if (ok) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             const double d = (double)c[i] - (double)cref[i];
@@ -404,15 +439,69 @@ __device__ __forceinline__ void tile_dct_stats(const float* tile, const float* s
     }
 }
 
-// Reduce the per-lane sums over the 16 frame columns; returns mean in s1 and std in s2.
+// Swap one tile's contribution: remove the unclamped columns `co`, add the clamped `cn`.
+__device__ __forceinline__ void stats_replace(const float (&cn)[8], const float (&co)[8], const float (&cref)[8],
+                                              bool ok, double (&s1)[8], double (&s2)[8]) {
+    if (ok) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const double dn = (double)cn[i] - (double)cref[i], dd = (double)co[i] - (double)cref[i];
+            s1[i] += dn - dd;
+            s2[i] += fma(dn, dn, -dd * dd);
+        }
+    }
+}
+
+// Wave minimum of a float, no LDS: DPP row scan, then the four row results via readlane.
+__device__ __forceinline__ float wave_min(float x) {
+    x = fminf(x, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), 0x111, 0xf, 0xf, false)));
+    x = fminf(x, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), 0x112, 0xf, 0xf, false)));
+    x = fminf(x, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), 0x114, 0xf, 0xf, false)));
+    x = fminf(x, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), 0x118, 0xf, 0xf, false)));
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 15));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 31));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 47));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63));
+    return fminf(fminf(r0, r1), fminf(r2, r3));
+}
+
+// Sum over the 16 lanes of each row (DPP row_shr scan, no LDS); the total lands in lane 15 of the row.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double x) {   // DPP move of a double; lanes without a source read 0
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double row_sum_d(double x) {
+    x += dpp_d<0x111>(x);   // row_shr:1
+    x += dpp_d<0x112>(x);   // row_shr:2
+    x += dpp_d<0x114>(x);   // row_shr:4
+    x += dpp_d<0x118>(x);   // row_shr:8
+    return x;
+}
+
+// Sum over the wave (rows via DPP, then the four row totals via readlane); uniform result.
+__device__ __forceinline__ double wave_sum_d(double x) {
+    x = row_sum_d(x);
+    double t = 0.0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        t += __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), 16 * r + 15),
+                              __builtin_amdgcn_readlane(__double2loint(x), 16 * r + 15));
+    return t;
+}
+
+// Wave maximum of a float (see wave_min).
+__device__ __forceinline__ float wave_max(float x) { return -wave_min(-x); }
+
+// Reduce the per-lane sums over the 16 frame columns; lane 15 of each row returns the
+// mean in s1 and the std in s2.
 __device__ __forceinline__ void finish_stats(int T, const float (&cref)[8], double (&s1)[8], double (&s2)[8]) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-#pragma unroll
-        for (int m = 1; m < 16; m <<= 1) {
-            s1[i] += __shfl_xor(s1[i], m, 64);
-            s2[i] += __shfl_xor(s2[i], m, 64);
-        }
+        s1[i] = row_sum_d(s1[i]);
+        s2[i] = row_sum_d(s2[i]);
         const double Td = (double)T;
         const double mean = (double)cref[i] + s1[i] / Td;
         double var = (s2[i] - s1[i] * s1[i] / Td) / Td;
@@ -426,17 +515,20 @@ __device__ __forceinline__ void zero_row(float* tile, int r, int lane) {
     for (int m = lane & 15; m < NMEL; m += 16) tile[r * NMEL + m] = 0.0f;
 }
 
-// Whole segment for one wave.  gscr: this wave's log-mel scratch (flat 16x128-float
-// tiles, float4 [tile][8][64]), able to hold `scr_tiles` tiles.
+// Whole segment for one wave.  gscr: this wave's log-mel scratch -- `scr_tiles` flat
+// 16x128-float tiles (float4 [tile][8][64]) followed by the pass-1 DCT columns of each
+// tile (float4 [tile][2][64]); tmins: per-tile log-mel minimum (LDS, one float per tile).
 template <int RING>
 __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, float* scr, float* tile,
-                              float4* gscr, int scr_tiles, int lane, const int (&lo)[8], double (&s1)[8],
-                              double (&s2)[8]) {
+                              float* tmins, float4* gscr, int scr_tiles, int lane, const int (&lo)[8],
+                              double (&s1)[8], double (&s2)[8], uint64_t* tim) {
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     const int T = 1 + v.len / HOP;
     const int ntile = (T + 15) >> 4;
     const int npass = (T + 3) >> 2;
     const bool park = ntile <= scr_tiles;
+    const int col = lane & 15;
+    float4* gcol = gscr + (int64_t)scr_tiles * 8 * 64;
     float cref[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
@@ -449,53 +541,86 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     }
     float4* tile4 = reinterpret_cast<float4*>(tile);
     for (int tile_i = 0; tile_i < ntile; ++tile_i) {
+        float tmin = INFINITY;
+        EWK_TS(t0);
 #pragma unroll 1
         for (int p = 0; p < 4; ++p) {
             const int pass = tile_i * 4 + p;
             if (pass < npass)
-                frame_pass(v, pass * 4, T, p * 4, pass + 1 < npass, smem, scr, tile, lane, lo, vmax, vmin);
+                frame_pass(v, pass * 4, T, p * 4, pass + 1 < npass, smem, scr, tile, lane, lo, vmax, tmin, tim);
             else   // rows of frames past T: zero (ignored by the statistics)
                 zero_row(tile, p * 4 + (lane >> 4), lane);
         }
         lds_order();
+        EWK_TS(t1);
+        EWK_TACC(0, t0, t1);
         if (park) {
             float4* dst = gscr + (int64_t)tile_i * 8 * 64 + lane;
 #pragma unroll
             for (int k = 0; k < 8; ++k) dst[k * 64] = tile4[k * 64 + lane];
         }
-        tile_dct_stats(tile, s_dct, tile_i, T, lane, cref, s1, s2);
-    }
-    // wave-wide log-mel max/min
+        float c[8];
+        tile_dct(tile, s_dct, lane, c);
+        if (tile_i == 0) {
 #pragma unroll
-    for (int m = 1; m < 64; m <<= 1) {
-        vmax = fmaxf(vmax, __shfl_xor(vmax, m, 64));
-        vmin = fminf(vmin, __shfl_xor(vmin, m, 64));
+            for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
+        }
+        stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
+        if (park) {
+            float4* dst = gcol + (int64_t)tile_i * 2 * 64 + lane;
+            dst[0] = make_float4(c[0], c[1], c[2], c[3]);
+            dst[64] = make_float4(c[4], c[5], c[6], c[7]);
+        }
+        vmin = fminf(vmin, tmin);
+        tmin = wave_min(tmin);
+        if (lane == 0) tmins[tile_i] = tmin;
+        EWK_TS(t2);
+        EWK_TACC(1, t1, t2);
     }
+    EWK_TS(t3);
+    // wave-wide log-mel max/min
+    vmax = wave_max(vmax);
+    vmin = wave_min(vmin);
     const float theta = vmax - 80.0f;
 #if !(EWK_ABLATE & 32)
     if (vmin < theta) {
-        // top_db clamp: redo the DCT + statistics from the parked log-mel tiles
-#pragma unroll
-        for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; }
+        lds_order();
         if (park) {
-            float4 nx[8];
+            // top_db clamp: only tiles holding a value below max - 80 dB change; swap
+            // their pass-1 contribution for the clamped one (parked log-mel + DCT columns)
+            int cur = 0;
+            while (cur < ntile && !(tmins[cur] < theta)) ++cur;
+            float4 nx[8], no0, no1;
+            if (cur < ntile) {
 #pragma unroll
-            for (int k = 0; k < 8; ++k) nx[k] = gscr[k * 64 + lane];
-            for (int tile_i = 0; tile_i < ntile; ++tile_i) {
+                for (int k = 0; k < 8; ++k) nx[k] = gscr[(int64_t)cur * 512 + k * 64 + lane];
+                no0 = gcol[(int64_t)cur * 128 + lane];
+                no1 = gcol[(int64_t)cur * 128 + 64 + lane];
+            }
+            while (cur < ntile) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
                     tile4[k * 64 + lane] = make_float4(fmaxf(nx[k].x, theta), fmaxf(nx[k].y, theta),
                                                        fmaxf(nx[k].z, theta), fmaxf(nx[k].w, theta));
+                const float co[8] = {no0.x, no0.y, no0.z, no0.w, no1.x, no1.y, no1.z, no1.w};
                 lds_order();
-                if (tile_i + 1 < ntile) {   // next tile's loads overlap this tile's MFMAs
-                    const float4* src = gscr + (int64_t)(tile_i + 1) * 8 * 64 + lane;
+                int nxt = cur + 1;
+                while (nxt < ntile && !(tmins[nxt] < theta)) ++nxt;
+                if (nxt < ntile) {   // next clamped tile's loads overlap this tile's MFMAs
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) nx[k] = src[k * 64];
+                    for (int k = 0; k < 8; ++k) nx[k] = gscr[(int64_t)nxt * 512 + k * 64 + lane];
+                    no0 = gcol[(int64_t)nxt * 128 + lane];
+                    no1 = gcol[(int64_t)nxt * 128 + 64 + lane];
                 }
-                tile_dct_stats(tile, s_dct, tile_i, T, lane, cref, s1, s2);
+                float cn[8];
+                tile_dct(tile, s_dct, lane, cn);
+                stats_replace(cn, co, cref, cur * 16 + col < T, s1, s2);
+                cur = nxt;
             }
         } else {
             // longer than the scratch: recompute the FFT with the clamp applied per tile
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; }
             {
                 float r[16];
                 stage_load(v, -NFFT / 2, lane, r);
@@ -520,12 +645,18 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
                                                        fmaxf(x.z, theta), fmaxf(x.w, theta));
                 }
                 lds_order();
-                tile_dct_stats(tile, s_dct, tile_i, T, lane, cref, s1, s2);
+                float c[8];
+                tile_dct(tile, s_dct, lane, c);
+                stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
             }
         }
     }
 #endif
+    EWK_TS(t4);
+    EWK_TACC(2, t3, t4);
     finish_stats(T, cref, s1, s2);
+    EWK_TS(t5);
+    EWK_TACC(3, t4, t5);
 }
 
 // ---- the score, exactly as WordMatcher.calculate_similarity evaluates it --------
@@ -602,11 +733,6 @@ __device__ double score_f32cand(const float* tm, const float* ts, const float* c
     return (double)(powf(percent, 1.5f) / 10.0f);
 }
 
-__device__ __forceinline__ double wave_sum_d(double x) {
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) x += __shfl_xor(x, m, 64);
-    return x;
-}
 
 // Fast-path finishes (the fp64 re-score keeps the reference's exact pow / sequential dots).
 __device__ __forceinline__ double score_f64_finish(double uu_m, double uu_s, double uv_m, double vv_m, double uv_s,
@@ -668,7 +794,8 @@ __global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__
     float* scr = reinterpret_cast<float*>(wbase + W_SCR);
     float* tile = reinterpret_cast<float*>(wbase + W_TILE);
     float* misc = reinterpret_cast<float*>(wbase + W_MISC);
-    float4* gscr = reinterpret_cast<float4*>(a.lm_scratch) + (int64_t)(blockIdx.x * WAVES + wave) * a.lm_tiles * 8 * 64;
+    float4* gscr = reinterpret_cast<float4*>(a.lm_scratch) + (int64_t)(blockIdx.x * WAVES + wave) * a.lm_tiles * 10 * 64;
+    float* tmins = reinterpret_cast<float*>(wbase + W_TMIN);
     int lo[8];   // first bin of this lane's bands j + 16 i
     {
         const int* sb = reinterpret_cast<const int*>(smem + L_BLO);
@@ -676,7 +803,14 @@ __global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__
         for (int i = 0; i < 8; ++i) lo[i] = sb[(lane & 15) + 16 * i];
     }
     // persistent waves pull segments from a work counter (ragged lengths balance)
+#if EWK_TIMING
+    uint64_t tim[17] = {};
+    EWK_TS(t_begin);
+#else
+    uint64_t* tim = nullptr;
+#endif
     for (;;) {
+        EWK_TS(ta);
         int idx = 0;
         if (lane == 0) idx = atomicAdd(a.work, 1);
         idx = __shfl(idx, 0, 64);
@@ -701,10 +835,13 @@ __global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__
         const SegSrc<RING> v = make_src<RING>(p, start, ring, len);
 
         double st1[8], st2[8];
-        segment_stats(v, smem, scr, tile, gscr, a.lm_tiles, lane, lo, st1, st2);
+        EWK_TS(tb);
+        EWK_TACC(4, ta, tb);
+        segment_stats(v, smem, scr, tile, tmins, gscr, a.lm_tiles, lane, lo, st1, st2, tim);
+        EWK_TS(tc);
 
         // ---- gather fp32-rounded mean/std into misc[0..19], misc[20..39]
-        if ((lane & 15) == 0) {
+        if ((lane & 15) == 15) {   // finish_stats leaves each row's totals in its lane 15
             const int h = lane >> 4;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -756,7 +893,17 @@ __global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__
             }
         }
         lds_order();
+        EWK_TS(td);
+        EWK_TACC(5, tc, td);
     }   // work loop
+#if EWK_TIMING
+    EWK_TS(t_end);
+    EWK_TACC(6, t_begin, t_end);
+    if (lane == 0) {
+        for (int i = 0; i < 17; ++i) if (i != 7) atomicAdd(&g_tim[i], (unsigned long long)tim[i]);
+        atomicAdd(&g_tim[7], 1ull);
+    }
+#endif
 }
 
 __global__ void k_advance(int32_t* ev_base, const int32_t* n_events) { *ev_base = *n_events; }
@@ -953,3 +1100,12 @@ hipError_t launch_score_f64(const Tables64* d_tab64, const ScoreArgs& a, int rin
 }
 
 }  // namespace ewk
+
+#if EWK_TIMING
+// per-phase cycle totals of k_score_f32 since the last call (timing builds only)
+extern "C" int ewk_debug_timing(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ewk::g_tim), 24 * sizeof(unsigned long long)) != hipSuccess) return -3;
+    unsigned long long z[24] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(ewk::g_tim), z, sizeof(z)) == hipSuccess ? 0 : -3;
+}
+#endif

@@ -29,3 +29,16 @@ ms /= k
 lib = os.path.basename(os.environ.get("EWK_LIB", "libewk.so"))
 print(f"{lib:28s} {ms:8.3f} ms  {frames/ms/1e6:7.3f} Gframes/s  frac={frames*640/(ms/1e3)/8e12:.4f}  "
       f"matches={int(match.sum())} nan={int(torch.isnan(score).sum())} s0={float(score[0]):.4f}")
+import ctypes
+lib = ctypes.CDLL(os.environ.get("EWK_LIB") or os.path.join(ROOT, "easywakeword_amd", "libewk.so"))
+if hasattr(lib, "ewk_debug_timing"):
+    buf = (ctypes.c_ulonglong * 24)()
+    lib.ewk_debug_timing(buf)      # reset
+    e.profile(False)
+    step(); torch.cuda.synchronize()
+    lib.ewk_debug_timing(buf)
+    names = ["frame passes", "tile park+dct+stats", "clamp pass", "finish_stats", "fetch+setup", "epilogue", "wave lifetime"]
+    w = max(1, buf[7])
+    print("  per-wave cycles: " + ", ".join(f"{n}={buf[i] / w:,.0f}" for i, n in enumerate(names)))
+    sub = ["window", "prefetch issue", "dft1+tw", "transposes", "dft2", "untangle+power", "mel+log", "tile writes", "stage store"]
+    print("  frame-pass split: " + ", ".join(f"{n}={buf[8 + i] / w:,.0f}" for i, n in enumerate(sub)))
