@@ -255,15 +255,14 @@ def main():
     sh = stream.cuda_stream
     assert sh != 0
     if world > 1:
-        g_score = [torch.empty_like(score) for _ in range(world)]
-        g_match = [torch.empty_like(match) for _ in range(world)]
+        from easywakeword_amd.shard import DecisionGather
+        gather = DecisionGather(score, match)   # tests/test_dist_gloo.py runs the same code over gloo
 
     def step():
         eng.score_device(pcm.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n_seg, mean.data_ptr(),
                          std.data_ptr(), score.data_ptr(), match.data_ptr(), sh)
         if world > 1:   # gather every rank's decisions to all (rank 0 runs the confirm stage)
-            dist.all_gather(g_score, score)
-            dist.all_gather(g_match, match)
+            gather(score, match)
 
     torch.cuda.synchronize()
     for _ in range(args.warmup):
