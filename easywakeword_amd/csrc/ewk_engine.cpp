@@ -90,6 +90,8 @@ struct ewk_engine {
     // streaming
     float* d_ring = nullptr;
     double* d_brms = nullptr;
+    double* d_sorted = nullptr;     // [streams][2][n_blocks] sorted block RMS (double-buffered)
+    PwTree* d_trees = nullptr;      // numpy pairwise-sum trees for the block and the last 0.1 s
     GateStream* d_st = nullptr;
     ewk_event* d_events = nullptr;
     int32_t* d_evc = nullptr;   // [0] count, [1] dropped, [2] scored watermark
@@ -99,7 +101,7 @@ struct ewk_engine {
     size_t h_stage_cap = 0;
     hipEvent_t h_stage_free = nullptr;   // recorded after the last DMA out of h_stage
     int64_t tick = 0;
-    int32_t lds_gate = 0;
+    int32_t gate_stage = 0;
 
     // measurement: (start, stop) event pairs per kernel family
     bool prof = false;
@@ -216,6 +218,8 @@ void ewk_destroy(ewk_engine* e) {
     e->push_stage.release();
     (void)hipFree(e->d_ring);
     (void)hipFree(e->d_brms);
+    (void)hipFree(e->d_sorted);
+    (void)hipFree(e->d_trees);
     (void)hipFree(e->d_st);
     (void)hipFree(e->d_events);
     (void)hipFree(e->d_evc);
@@ -295,14 +299,30 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
         if ((err = hipMalloc(&e->d_ring, ring_bytes)) != hipSuccess) return bail(err, "ring");
         if ((err = hipMalloc(&e->d_brms, (size_t)n_streams * std::max(1, e->n_blocks) * sizeof(double))) != hipSuccess)
             return bail(err, "block rms");
+        if ((err = hipMalloc(&e->d_sorted, (size_t)n_streams * 2 * std::max(1, e->n_blocks) * sizeof(double))) !=
+            hipSuccess)
+            return bail(err, "sorted block rms");
         if ((err = hipMalloc(&e->d_st, (size_t)n_streams * sizeof(GateStream))) != hipSuccess) return bail(err, "state");
+        {
+            std::vector<PwTree> tr(kNumTrees);
+            const int64_t lens[2] = {c.block, e->n_last};
+            for (int k = 0; k < 2; ++k) {
+                const int64_t n = std::min<int64_t>(lens[k], e->ring_len);
+                build_pw_tree(n > kPwChunk ? kPwChunk : 0, &tr[2 * k]);
+                const int64_t r = n % kPwChunk;
+                build_pw_tree((int)(n > kPwChunk ? (r ? r : kPwChunk) : n), &tr[2 * k + 1]);
+            }
+            if ((err = hipMalloc(&e->d_trees, kNumTrees * sizeof(PwTree))) != hipSuccess) return bail(err, "trees");
+            if ((err = hipMemcpy(e->d_trees, tr.data(), kNumTrees * sizeof(PwTree), hipMemcpyHostToDevice)) != hipSuccess)
+                return bail(err, "trees");
+        }
         e->ev_cap = std::max(4096, 4 * n_streams);
         if ((err = reserve_rescore(e, e->ev_cap)) != hipSuccess) return bail(err, "rescore list");
         if ((err = reserve_lm(e, e->ev_cap, 1)) != hipSuccess) return bail(err, "log-mel scratch");
         if ((err = hipMalloc(&e->d_events, (size_t)e->ev_cap * sizeof(ewk_event))) != hipSuccess)
             return bail(err, "events");
         if ((err = hipMalloc(&e->d_evc, 4 * sizeof(int32_t))) != hipSuccess) return bail(err, "event counters");
-        e->lds_gate = gate_lds_per_wave(e->n_blocks);
+        e->gate_stage = gate_stage_len(c.block, e->n_last);
         int rc = ewk_reset_streams(e);
         if (rc != EWK_OK) {
             std::string m = g_err;
@@ -649,12 +669,14 @@ static int push_impl(ewk_engine* e, const float* pcm, int64_t stride, int64_t ti
         g.ring = e->d_ring;
         g.ring_len = e->ring_len;
         g.block_rms = e->d_brms;
+        g.sorted_rms = e->d_sorted;
+        g.trees = e->d_trees;
         g.st = e->d_st;
         g.block = e->cfg.block;
         g.n_blocks = e->n_blocks;
         g.n_last = e->n_last;
         g.sample_rate = e->cfg.sample_rate;
-        g.lds_per_wave = e->lds_gate;
+        g.stage = e->gate_stage;
         g.tick_seconds = e->cfg.tick_seconds;
         g.pre_speech_silence = e->cfg.pre_speech_silence;
         g.speech_duration_min = e->cfg.speech_duration_min;

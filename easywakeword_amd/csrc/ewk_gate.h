@@ -25,9 +25,36 @@ struct GateStream {
     int32_t state;
     int32_t started;
     int32_t last_silent;
-    int32_t filled;          // block RMS cache valid
+    int32_t filled;          // block RMS cache + sorted copy valid
     int32_t reentries;
+    int32_t sorted_sel;      // which of the two sorted_rms halves is current
+    int32_t pad;
 };
+
+// numpy's pairwise summation order (np.add.reduce on a contiguous float64 array,
+// numpy/_core/src/umath/loops_utils.h.src pairwise_sum) for ONE chunk of n <= 8192
+// elements, flattened on the host: leaves of <= 128 elements (8-accumulator loop),
+// and the internal nodes grouped by height so a wave evaluates each level in parallel.
+// Node ids: leaves 0..n_leaves-1, internal node k has id n_leaves + k.
+constexpr int kPwChunk = 8192;
+constexpr int kPwMaxLeaves = 256;
+constexpr int kPwMaxLevels = 16;
+struct PwTree {
+    int32_t n;
+    int32_t n_leaves;
+    int32_t n_levels;
+    int32_t pad;
+    int16_t leaf_start[kPwMaxLeaves];
+    int16_t leaf_len[kPwMaxLeaves];
+    int16_t left[kPwMaxLeaves];     // internal node k = val[left[k]] + val[right[k]]
+    int16_t right[kPwMaxLeaves];
+    int16_t level_end[kPwMaxLevels];   // internal nodes of height h+1: [level_end[h-1], level_end[h])
+};
+// The gate's summation lengths: the callback block (frame_size) and the last 0.1 s,
+// each as a full-chunk tree (n = 8192, used when the length exceeds one chunk) and
+// the tree of the final (or only) chunk.
+enum { kTreeBlockFull = 0, kTreeBlockRem = 1, kTreeLastFull = 2, kTreeLastRem = 3, kNumTrees = 4 };
+void build_pw_tree(int n, PwTree* t);
 
 struct GateArgs {
     const float* pcm;        // stream s, tick t: pcm[s*stride + t*tick_stride + i]
@@ -38,13 +65,15 @@ struct GateArgs {
     int64_t tick0;           // ticks already delivered
     float* ring;             // [n_streams][ring_len]
     int64_t ring_len;
-    double* block_rms;       // [n_streams][n_blocks]
+    double* block_rms;       // [n_streams][n_blocks] RMS of each physical block
+    double* sorted_rms;      // [n_streams][2][n_blocks] the same values, ascending (double-buffered)
     GateStream* st;
+    const PwTree* trees;     // kNumTrees
     int32_t block;           // callback frame_size
     int32_t n_blocks;        // ring_len // block
     int64_t n_last;          // int(0.1 * sample_rate)
     int32_t sample_rate;
-    int32_t lds_per_wave;
+    int32_t stage;           // per-wave LDS sample staging (floats); 0 = read the ring directly
     double tick_seconds;
     double pre_speech_silence, speech_duration_min, speech_duration_max, post_speech_silence;
     double padding, max_segment_seconds, reentry_timeout, min_threshold;
@@ -55,6 +84,7 @@ struct GateArgs {
 };
 
 hipError_t launch_gate(const GateArgs& g, hipStream_t s);
-int gate_lds_per_wave(int n_blocks);
+// per-wave sample staging length for a config (0 when the lengths exceed the LDS budget)
+int gate_stage_len(int block, int64_t n_last);
 
 }  // namespace ewk

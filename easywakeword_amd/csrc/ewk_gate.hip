@@ -9,10 +9,27 @@
 // All comparisons are float64 and bit-identical to the reference's numpy
 // arithmetic: squares of float32 samples are exact in float64, sums follow
 // numpy's pairwise order (chunks of 8192, 8-accumulator leaves of <= 128,
-// split at n2 = n/2 - (n/2)%8), the percentile follows numpy 2.2's "linear"
-// method (_compute_virtual_index / _lerp), and the clock is tick * tick_seconds.
+// split at n2 = n/2 - (n/2)%8; the tree is flattened once on the host and
+// evaluated level by level across the wave), the percentile follows numpy
+// 2.2's "linear" method (_compute_virtual_index / _lerp), and the clock is
+// tick * tick_seconds.
+//
+// Incremental state per stream (the reference recomputes everything per tick):
+//   * block_rms[b]: RMS of physical block b, refreshed only for the blocks the
+//     tick's samples overlap (the other blocks hold the same samples, hence the
+//     same value);
+//   * sorted_rms: the same multiset kept sorted (one remove + one insert per
+//     refreshed block, wave-parallel), so np.percentile(all_rms, 25) is a lookup
+//     of the two order statistics it interpolates;
+//   * the tick's samples are staged in LDS, so the refreshed block and the last
+//     0.1 s window are summed without re-reading the ring; when the window is the
+//     refreshed block (aligned ticks, n_last == block) its sum is reused.
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
 
 #include "ewk_gate.h"
 
@@ -21,88 +38,82 @@
 
 namespace ewk {
 
-constexpr int kMaxLeaves = 256;   // n <= 8192 per chunk -> <= 128 leaves
-
-// ---- numpy pairwise sum of squares, exact order --------------------------------
-// Leaves of chunk [0, n): depth-first, left to right.  Built by every lane
-// identically (uniform control flow, registers only).
-struct LeafList {
-    int32_t start[kMaxLeaves];
-    int32_t len[kMaxLeaves];
-    int32_t count;
-};
-
-__device__ __forceinline__ int split_point(int n) {
+// ---- host: flatten numpy's pairwise recursion for one chunk --------------------
+static int split_point(int n) {
     int n2 = n / 2;
     n2 -= n2 % 8;
     return n2;
 }
 
-// Enumerate leaves of pw(n) into LDS (lane 0) -- iterative DFS.
-__device__ void build_leaves(int n, int32_t* lstart, int32_t* llen, int32_t* lcount) {
-    int st_s[32], st_n[32];
-    int sp = 0, cnt = 0;
-    st_s[sp] = 0;
-    st_n[sp] = n;
-    ++sp;
-    while (sp > 0) {
-        --sp;
-        const int s = st_s[sp], m = st_n[sp];
+void build_pw_tree(int n, PwTree* t) {
+    memset(t, 0, sizeof(*t));
+    t->n = n;
+    if (n <= 0) return;
+    struct Node { int a, b, h; };   // children as tagged ids: >= 0 leaf, < 0 internal (-1 - index)
+    std::vector<Node> inner;
+    int nleaf = 0;
+    // returns tagged id and height
+    struct R { int id, h; };
+    auto rec = [&](auto&& self, int s, int m) -> R {
         if (m <= 128) {
-            lstart[cnt] = s;
-            llen[cnt] = m;
-            ++cnt;
-        } else {
-            const int n2 = split_point(m);
-            // push right first so the left subtree is visited first
-            st_s[sp] = s + n2; st_n[sp] = m - n2; ++sp;
-            st_s[sp] = s;      st_n[sp] = n2;     ++sp;
+            t->leaf_start[nleaf] = (int16_t)s;
+            t->leaf_len[nleaf] = (int16_t)m;
+            return R{nleaf++, 0};
         }
+        const int n2 = split_point(m);
+        const R a = self(self, s, n2);
+        const R b = self(self, s + n2, m - n2);
+        inner.push_back(Node{a.id, b.id, std::max(a.h, b.h) + 1});
+        return R{-1 - (int)(inner.size() - 1), std::max(a.h, b.h) + 1};
+    };
+    rec(rec, 0, n);
+    t->n_leaves = nleaf;
+    // order internal nodes by height (children always lower), keep creation order within a level
+    std::vector<int> order(inner.size());
+    for (size_t i = 0; i < inner.size(); ++i) order[i] = (int)i;
+    std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return inner[x].h < inner[y].h; });
+    std::vector<int> pos(inner.size());
+    for (size_t k = 0; k < order.size(); ++k) pos[order[k]] = (int)k;
+    auto node_id = [&](int tag) { return tag >= 0 ? tag : nleaf + pos[-1 - tag]; };
+    int levels = 0;
+    for (size_t k = 0; k < order.size(); ++k) {
+        const Node& nd = inner[order[k]];
+        t->left[k] = (int16_t)node_id(nd.a);
+        t->right[k] = (int16_t)node_id(nd.b);
+        t->level_end[nd.h - 1] = (int16_t)(k + 1);
+        levels = nd.h;
     }
-    *lcount = cnt;
+    t->n_levels = levels;
 }
 
-// Recombine leaf sums in the recursion's post-order: pw(n) = pw(left) + pw(right).
-__device__ double combine_leaves(int n, const double* leaf, int& li) {
-    // explicit stack emulating: f(m) = m<=128 ? leaf[li++] : f(n2) + f(m-n2)
-    int st_n[32];
-    int st_state[32];
-    double st_val[32];
-    int sp = 0;
-    st_n[0] = n;
-    st_state[0] = 0;
-    sp = 1;
-    double ret = 0.0;
-    while (sp > 0) {
-        const int top = sp - 1;
-        const int m = st_n[top];
-        if (m <= 128) {
-            ret = leaf[li++];
-            --sp;
-            // deliver ret to parent
-            while (sp > 0) {
-                const int p = sp - 1;
-                if (st_state[p] == 1) {         // left finished -> store, go right
-                    st_val[p] = ret;
-                    st_state[p] = 2;
-                    st_n[sp] = st_n[p] - split_point(st_n[p]);
-                    st_state[sp] = 0;
-                    ++sp;
-                    break;
-                } else {                        // right finished -> combine
-                    ret = st_val[p] + ret;
-                    --sp;
-                }
-            }
-        } else {
-            st_state[top] = 1;
-            st_n[sp] = split_point(m);
-            st_state[sp] = 0;
-            ++sp;
-        }
-    }
-    return ret;
+int gate_stage_len(int block, int64_t n_last) {
+    const int64_t m = std::max<int64_t>(block, n_last);
+    if (m > 4096) return 0;              // long callbacks: sum straight from the ring
+    return (int)((m + 3) & ~3);
 }
+
+// ---- device ---------------------------------------------------------------------
+__device__ __forceinline__ void wave_sync() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
+struct LdsSrc {
+    const float* p;
+    __device__ __forceinline__ float operator()(int i) const { return p[i]; }
+};
+
+struct RingSrc {
+    const float* ring;
+    int32_t first;   // physical index of element 0
+    int32_t R;
+    __device__ __forceinline__ float operator()(int i) const {
+        int k = first + i;
+        if (k >= R) k -= R;
+        return ring[k];
+    }
+};
 
 // Sum of squares of one leaf (n <= 128) exactly as numpy's inner loop.
 template <typename Src>
@@ -126,55 +137,39 @@ __device__ __forceinline__ double leaf_sumsq(const Src& src, int s, int n) {
     return res;
 }
 
-// numpy np.add.reduce(x**2) over n float32 samples read through src(i), wave-cooperative.
-// scratch: >= 2*kMaxLeaves ints + kMaxLeaves doubles of per-wave LDS.
+// One chunk (n = t->n elements of src) in numpy's pairwise order, wave-parallel.
+// val: per-wave LDS scratch of 2 * kPwMaxLeaves doubles.  Uniform result.
 template <typename Src>
-__device__ double wave_pairwise_sumsq(const Src& src, int n, int lane, int32_t* lstart, int32_t* llen,
-                                      int32_t* lcount, double* lsum) {
+__device__ double tree_sumsq(const Src& src, const PwTree* t, int lane, double* val) {
+    const int L = t->n_leaves;
+    for (int l = lane; l < L; l += 64) val[l] = leaf_sumsq(src, t->leaf_start[l], t->leaf_len[l]);
+    wave_sync();
+    int b = 0;
+    for (int h = 0; h < t->n_levels; ++h) {
+        const int e = t->level_end[h];
+        for (int k = b + lane; k < e; k += 64) val[L + k] = val[t->left[k]] + val[t->right[k]];
+        b = e;
+        wave_sync();
+    }
+    const double r = (L == 1) ? val[0] : val[L + b - 1];   // the root is the last internal node
+    wave_sync();
+    return r;
+}
+
+// np.add.reduce(x**2) over n samples: chunks of 8192 accumulated from 0.0.
+template <typename MakeSrc>
+__device__ double pw_sumsq(const MakeSrc& make, int n, const PwTree* full, const PwTree* rem, int lane,
+                           double* val) {
     double acc = 0.0;
-    for (int c0 = 0; c0 < n; c0 += 8192) {
-        const int cn = min(8192, n - c0);
-        if (lane == 0) build_leaves(cn, lstart, llen, lcount);
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-        const int nl = *lcount;
-        for (int l = lane; l < nl; l += 64) lsum[l] = leaf_sumsq(src, c0 + lstart[l], llen[l]);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        double part = 0.0;
-        if (lane == 0) {
-            int li = 0;
-            part = combine_leaves(cn, lsum, li);
-        }
-        part = __shfl(part, 0, 64);
-        acc += part;
-        asm volatile("" ::: "memory");
+    for (int c0 = 0; c0 < n; c0 += kPwChunk) {
+        const int cn = min(kPwChunk, n - c0);
+        acc += tree_sumsq(make(c0), cn == full->n ? full : rem, lane, val);
     }
     return acc;
 }
 
-struct RingSrc {
-    const float* ring;
-    int64_t first;   // physical index of element 0
-    int64_t R;
-    __device__ __forceinline__ float operator()(int i) const {
-        int64_t k = first + i;
-        if (k >= R) k -= R;
-        return ring[k];
-    }
-};
-
-// numpy percentile(v, 25) ("linear"), v of length nb held in LDS.
-__device__ double wave_percentile25(const double* v, int nb, int lane, double* sel) {
-    // virtual index = n*q + (alpha + q*(1-alpha-beta)) - 1, alpha = beta = 1, q = 0.25
-    const double q = 0.25;
-    const double vi = (double)nb * q + (1.0 + q * (1.0 - 1.0 - 1.0)) - 1.0;
-    double prevd = floor(vi);
-    int prev = (int)prevd, next = prev + 1;
-    if (vi >= (double)(nb - 1)) { prev = nb - 1; next = nb - 1; }
-    if (vi < 0.0) { prev = 0; next = 0; }
-    const double gamma = vi - prevd;
-    // rank selection with index tie-break
+// First fill: rank-sort v (global, nb values) into dst (global).
+__device__ void rank_sort(const double* v, double* dst, int nb, int lane) {
     for (int i = lane; i < nb; i += 64) {
         const double x = v[i];
         int r = 0;
@@ -182,12 +177,41 @@ __device__ double wave_percentile25(const double* v, int nb, int lane, double* s
             const double y = v[k];
             r += (y < x) || (y == x && k < i);
         }
-        if (r == prev) sel[0] = x;
-        if (r == next) sel[1] = x;
+        dst[r] = x;
     }
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    const double a = sel[0], b = sel[1];
+}
+
+// src (sorted) with one occurrence of vo replaced by vn -> dst (sorted).
+// Returns false when vo is absent (cache inconsistent: caller re-sorts).
+__device__ bool sorted_replace(const double* src, double* dst, int nb, double vo, double vn, int lane) {
+    int pos = nb;
+    for (int i = lane; i < nb; i += 64)
+        if (src[i] == vo) { pos = i; break; }
+    for (int m = 1; m < 64; m <<= 1) pos = min(pos, __shfl_xor(pos, m, 64));
+    if (pos >= nb) return false;
+    int cnt = 0;
+    for (int i = lane; i < nb; i += 64) cnt += (i != pos && src[i] < vn) ? 1 : 0;
+    for (int m = 1; m < 64; m <<= 1) cnt += __shfl_xor(cnt, m, 64);
+    for (int i = lane; i < nb; i += 64) {
+        if (i == pos) continue;
+        const int i1 = i < pos ? i : i - 1;
+        dst[i1 < cnt ? i1 : i1 + 1] = src[i];
+    }
+    if (lane == 0) dst[cnt] = vn;
+    return true;
+}
+
+// numpy.percentile(v, 25) ("linear") from the sorted copy.
+__device__ __forceinline__ double percentile25_sorted(const double* sorted, int nb) {
+    // virtual index = n*q + (alpha + q*(1-alpha-beta)) - 1, alpha = beta = 1, q = 0.25
+    const double q = 0.25;
+    const double vi = (double)nb * q + (1.0 + q * (1.0 - 1.0 - 1.0)) - 1.0;
+    const double prevd = floor(vi);
+    int prev = (int)prevd, next = prev + 1;
+    if (vi >= (double)(nb - 1)) { prev = nb - 1; next = nb - 1; }
+    if (vi < 0.0) { prev = 0; next = 0; }
+    const double gamma = vi - prevd;
+    const double a = sorted[prev], b = sorted[next];
     // numpy _lerp: a + (b-a)*t, replaced by b - (b-a)*(1-t) where t >= 0.5
     const double d = b - a;
     double r = a + d * gamma;
@@ -198,23 +222,35 @@ __device__ double wave_percentile25(const double* v, int nb, int lane, double* s
 __global__ __launch_bounds__(256) void k_gate_ticks(GateArgs g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // pairwise trees (shared by the workgroup)
+    PwTree* trees = reinterpret_cast<PwTree*>(smem);
+    {
+        const int4* src = reinterpret_cast<const int4*>(g.trees);
+        int4* dst = reinterpret_cast<int4*>(smem);
+        for (int i = threadIdx.x; i < (int)(kNumTrees * sizeof(PwTree) / 16); i += blockDim.x) dst[i] = src[i];
+    }
+    __syncthreads();
     const int s = blockIdx.x * 4 + wave;
     if (s >= g.n_streams) return;
-    unsigned char* w = smem + wave * g.lds_per_wave;
-    int32_t* lstart = reinterpret_cast<int32_t*>(w);
-    int32_t* llen = lstart + kMaxLeaves;
-    int32_t* lcount = llen + kMaxLeaves;                           // + 4 ints pad
-    double* lsum = reinterpret_cast<double*>(lcount + 4);
-    double* sel = lsum + kMaxLeaves;                               // 2 doubles
-    double* brms = sel + 2;                                        // nb doubles
+    const size_t tree_bytes = (kNumTrees * sizeof(PwTree) + 15) & ~(size_t)15;
+    const size_t per_wave = (size_t)2 * kPwMaxLeaves * 8 + (size_t)g.stage * 4;
+    unsigned char* w = smem + tree_bytes + wave * per_wave;
+    double* val = reinterpret_cast<double*>(w);
+    float* stage = reinterpret_cast<float*>(w + 2 * kPwMaxLeaves * 8);
 
-    const int64_t R = g.ring_len;
+    const int R = (int)g.ring_len;
     const int fs = g.block;
     const int nb = g.n_blocks;
+    const int nl = (int)min<int64_t>(g.n_last, g.ring_len);
     float* ring = g.ring + (int64_t)s * R;
     GateStream st = g.st[s];
-    // per-stream block RMS cache lives in global memory; stage in LDS when full
     double* grms = g.block_rms + (int64_t)s * nb;
+    double* sorted2 = g.sorted_rms + (int64_t)s * 2 * nb;
+    const PwTree* tbf = trees + kTreeBlockFull;
+    const PwTree* tbr = trees + kTreeBlockRem;
+    const PwTree* tlf = trees + kTreeLastFull;
+    const PwTree* tlr = trees + kTreeLastRem;
+    const bool staged = g.stage >= fs && g.stage >= nl;
 
     for (int t = 0; t < g.n_ticks; ++t) {
         const int64_t tick = g.tick0 + t + 1;                    // tick being delivered
@@ -226,60 +262,102 @@ __global__ __launch_bounds__(256) void k_gate_ticks(GateArgs g) {
             if (st.last_silent) { st.state = kInSilence; st.silence_start = t_prev; }
             st.reentries += 1;
         }
-        // ---- a1: ingest `fs` samples at the write pointer
+        // ---- a1: ingest `fs` samples at the write pointer (and stage them in LDS)
         const float* src = g.pcm + (int64_t)s * g.stride + (int64_t)t * g.tick_stride;
-        const int64_t p0 = st.pointer;
+        const int p0 = st.pointer;
         for (int i = lane; i < fs; i += 64) {
-            int64_t k = p0 + i;
+            const float x = src[i];
+            int k = p0 + i;
             if (k >= R) k -= R;
-            ring[k] = src[i];
+            ring[k] = x;
+            if (staged) stage[i] = x;
         }
         __threadfence_block();
-        __builtin_amdgcn_wave_barrier();
+        wave_sync();
+        const bool wrapped = p0 + fs > R;
         st.pointer = (int32_t)((p0 + fs) % R);
-        st.collected = min(st.collected + (int64_t)fs, R);
+        st.collected = min(st.collected + (int64_t)fs, (int64_t)R);
         const bool full = st.collected >= R;
+        // block sum of the window when it coincides with a refreshed block
+        double reuse_sum = 0.0;
+        bool have_reuse = false;
         // ---- a2: threshold over the physical blocks (only once the ring is full)
         if (full) {
-            // refresh the physical blocks overlapping the written range [p0, p0+fs)
-            // (mod R); all blocks on the first fill (nothing was cached before)
-            auto refresh = [&](int64_t a0, int64_t a1) {   // [a0, a1) inside [0, R)
-                const int b0 = (int)(a0 / fs);
-                const int b1 = (int)((a1 - 1) / fs);
-                for (int b = b0; b <= b1 && b < nb; ++b) {
-                    RingSrc rs{ring, (int64_t)b * fs, R};
-                    const double sum = wave_pairwise_sumsq(rs, fs, lane, lstart, llen, lcount, lsum);
+            auto block_sum = [&](int b) -> double {
+                const int a0 = b * fs;
+                if (staged && a0 == p0)   // the block is exactly this tick's samples
+                    return pw_sumsq([&](int c0) { return LdsSrc{stage + c0}; }, fs, tbf, tbr, lane, val);
+                return pw_sumsq([&](int c0) { return RingSrc{ring, a0 + c0, R}; }, fs, tbf, tbr, lane, val);
+            };
+            if (!st.filled) {
+                for (int b = 0; b < nb; ++b) {
+                    const double sum = block_sum(b);
                     if (lane == 0) grms[b] = sqrt(sum / (double)fs);
                 }
-            };
-            if (!st.filled) refresh(0, (int64_t)nb * fs);
-            else if (p0 + fs <= R) refresh(p0, p0 + fs);
-            else { refresh(p0, R); refresh(0, p0 + fs - R); }
-            st.filled = 1;
+                __threadfence_block();
+                wave_sync();
+                rank_sort(grms, sorted2, nb, lane);
+                st.sorted_sel = 0;
+                st.filled = 1;
+            } else {
+                // refresh the physical blocks overlapping the written range [p0, p0+fs) (mod R)
+                auto refresh = [&](int a0, int a1) {   // [a0, a1) inside [0, R)
+                    const int b0 = a0 / fs;
+                    const int b1 = (a1 - 1) / fs;
+                    for (int b = b0; b <= b1 && b < nb; ++b) {
+                        const double sum = block_sum(b);
+                        const double v = sqrt(sum / (double)fs);
+                        if (nl == fs && b * fs + fs == (int)st.pointer + (st.pointer == 0 ? R : 0)) {
+                            reuse_sum = sum;
+                            have_reuse = true;
+                        }
+                        const double vo = grms[b];
+                        if (lane == 0) grms[b] = v;
+                        const double* cur = sorted2 + (int64_t)st.sorted_sel * nb;
+                        double* nxt = sorted2 + (int64_t)(st.sorted_sel ^ 1) * nb;
+                        __threadfence_block();
+                        wave_sync();
+                        if (!sorted_replace(cur, nxt, nb, vo, v, lane)) {
+                            __threadfence_block();
+                            wave_sync();
+                            rank_sort(grms, nxt, nb, lane);
+                        }
+                        st.sorted_sel ^= 1;
+                        __threadfence_block();
+                        wave_sync();
+                    }
+                };
+                if (!wrapped) refresh(p0, p0 + fs);
+                else { refresh(p0, R); refresh(0, p0 + fs - R); }
+            }
             __threadfence_block();
-            __builtin_amdgcn_wave_barrier();
-            for (int i = lane; i < nb; i += 64) brms[i] = grms[i];
-            asm volatile("" ::: "memory");
-            __builtin_amdgcn_wave_barrier();
-            const double p25 = wave_percentile25(brms, nb, lane, sel);
+            wave_sync();
+            const double p25 = percentile25_sorted(sorted2 + (int64_t)st.sorted_sel * nb, nb);
             const double thr = p25 * 1.5;
             // Python max(new, MIN): MIN only if MIN > new
             st.threshold = (g.min_threshold > thr) ? g.min_threshold : thr;
         }
         // ---- a3: is_silent(): RMS of the last n_last samples < threshold
         bool silent = true;
-        {
-            int64_t nl = g.n_last;
-            if (nl > R) nl = R;
-            if (nl > 0) {
-                int64_t first = (int64_t)st.pointer - nl;
+        if (nl > 0) {
+            double sum;
+            if (have_reuse) {
+                sum = reuse_sum;
+            } else if (staged && nl <= fs) {   // the window lies in this tick's samples
+                const float* base = stage + (fs - nl);
+                sum = pw_sumsq([&](int c0) { return LdsSrc{base + c0}; }, nl, tlf, tlr, lane, val);
+            } else {
+                int first = st.pointer - nl;
                 if (first < 0) first += R;
-                RingSrc rs{ring, first, R};
-                const double sum = wave_pairwise_sumsq(rs, (int)nl, lane, lstart, llen, lcount, lsum);
-                const double rms = sqrt(sum / (double)nl);
-                st.last_rms = rms;
-                silent = rms < st.threshold;
+                sum = pw_sumsq([&](int c0) {
+                    int f = first + c0;
+                    if (f >= R) f -= R;
+                    return RingSrc{ring, f, R};
+                }, nl, tlf, tlr, lane, val);
             }
+            const double rms = sqrt(sum / (double)nl);
+            st.last_rms = rms;
+            silent = rms < st.threshold;
         }
         st.last_silent = silent;
         st.tick = tick;
@@ -360,13 +438,10 @@ __global__ __launch_bounds__(256) void k_gate_ticks(GateArgs g) {
 hipError_t launch_gate(const GateArgs& g, hipStream_t s) {
     if (g.n_streams <= 0 || g.n_ticks <= 0) return hipSuccess;
     const int grid = (g.n_streams + 3) / 4;
-    hipLaunchKernelGGL(k_gate_ticks, dim3(grid), dim3(256), 4 * g.lds_per_wave, s, g);
+    const size_t tree_bytes = (kNumTrees * sizeof(PwTree) + 15) & ~(size_t)15;
+    const size_t per_wave = (size_t)2 * kPwMaxLeaves * 8 + (size_t)g.stage * 4;
+    hipLaunchKernelGGL(k_gate_ticks, dim3(grid), dim3(256), tree_bytes + 4 * per_wave, s, g);
     return hipGetLastError();
-}
-
-int gate_lds_per_wave(int n_blocks) {
-    const int bytes = kMaxLeaves * 4 * 2 + 16 + kMaxLeaves * 8 + 16 + n_blocks * 8;
-    return (bytes + 15) & ~15;
 }
 
 }  // namespace ewk
