@@ -298,6 +298,13 @@ def main():
 
     kernel_s = (k_ms / max(1, k_n)) / 1e3
     achieved = frames * BYTES_PER_FRAME / kernel_s / 1e9
+    traffic, traffic_src = None, None
+    tf = os.path.join(ROOT, "profiles", "traffic_k_score_f32.json")
+    if os.path.exists(tf):   # PMC-measured HBM bytes/frame of this kernel (scripts/gpu_round.sh pmc)
+        with open(tf) as fh:
+            t = json.load(fh)
+        traffic = t["traffic_bytes_per_frame"] * frames / 1e9
+        traffic_src = f"profiles/traffic_k_score_f32.json ({t['segments']} segments, {t['method']})"
 
     out = {
         "metric": METRIC,
@@ -327,7 +334,9 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "GB per launch",
+            "traffic_source": traffic_src,
             "kernel_ms": kernel_s * 1e3,
             "launches": k_n,
             "algorithmic_bytes_per_launch": frames * BYTES_PER_FRAME,

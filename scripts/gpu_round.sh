@@ -24,3 +24,11 @@ if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   rc=$?; echo "rocprof rc=$rc"; tail -5 "$R/gpurun_out/prof.log"
   find "$R/gpurun_out/prof" -name "*stats*" | head
 fi
+if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
+  R="${GRAFT_REPO_ROOT:-/root/repo}"
+  bash "$R/scripts/pmc.sh" "$R/easywakeword_amd/libewk.so" 65536 bench "FETCH_SIZE" "WRITE_SIZE" \
+     "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY" \
+     "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES" \
+     "SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE"
+  rc=$?; echo "pmc rc=$rc"; [ $rc -eq 0 ] || exit $rc
+fi

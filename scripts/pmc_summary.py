@@ -1,6 +1,7 @@
 """Summarise rocprofv3 --pmc passes (scripts/pmc.sh) for k_score_f32 into one text report.
 
-Usage: python scripts/pmc_summary.py gpurun_out/pmc_<tag> <n_segments> > profiles/rNN_<tag>_pmc.txt
+Usage: python scripts/pmc_summary.py gpurun_out/pmc_<tag> <n_segments> [traffic.json] > profiles/rNN_<tag>_pmc.txt
+(traffic.json: HBM bytes per launch / per frame for bench.py's roofline.traffic)
 
 Units (MI355X_MICROARCH.md, "s_memtime tick vs SQ PMC units" and the HBM section):
 SQ_WAVE_CYCLES / SQ_ACTIVE_INST_* / SQ_WAIT_* count quad-cycles; FETCH_SIZE / WRITE_SIZE are KB,
@@ -75,7 +76,15 @@ def main():
               f"write {write / 1e9:.3f} GB, total {(fetch + write) / 1e9:.3f} GB")
         print(f"algorithmic bytes per launch (640 B/frame): {alg / 1e9:.3f} GB; "
               f"traffic/algorithmic = {(fetch + write) / alg:.2f}")
-        print(f"  (write = parked log-mel tiles for the top_db pass, 512 B/frame; their re-read is in fetch)")
+        print(f"  (write = parked log-mel tiles + DCT columns for the top_db pass; their re-read is in fetch)")
+        if len(sys.argv) > 3:
+            import json
+            with open(sys.argv[3], "w") as fh:
+                json.dump({"kernel": "k_score_f32", "segments": n, "frames": frames,
+                           "fetch_bytes": fetch, "write_bytes": write, "traffic_bytes": fetch + write,
+                           "traffic_bytes_per_frame": (fetch + write) / frames,
+                           "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE, separate passes, "
+                                     "median over dispatches of scripts/mb_score.py"}, fh, indent=1)
 
 
 if __name__ == "__main__":
