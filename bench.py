@@ -152,15 +152,58 @@ def cpu_baseline(host_pcm, lengths, offsets, seconds):
                       f"{procs} processes x ~{seconds:.0f} s, OMP_NUM_THREADS=1"}
 
 
+def _cpu_stream_worker(args):
+    """Faithful CPU level 1 + level 2 (oracle/gate_ref.py DetectorRef + mfcc_ref scoring of every
+    emitted segment) on one synthetic stream of the streaming bench's recipe, ~`seconds` of work."""
+    seed, seconds = args
+    os.environ["OMP_NUM_THREADS"] = "1"
+    from oracle import gate_ref, mfcc_ref
+    word = load_word()
+    tm, ts = mfcc_ref.extract_mfcc(word)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    P = 160 * 1600
+    pcm = (rng.standard_normal(P) * rng.uniform(1e-4, 3e-3)).astype(np.float32)
+    for e in range(5):
+        pos = e * P // 5 + int(rng.integers(0, 8000))
+        src = word[::-1] if rng.random() < 0.3 else word
+        pcm[pos:pos + len(word)] += (src * rng.uniform(0.3, 2.0)).astype(np.float32)
+    det = gate_ref.DetectorRef(gate_ref.GateConfig(), keep_audio=True)
+    t0 = time.perf_counter()
+    ticks = 0
+    while time.perf_counter() - t0 < seconds:
+        k = ticks % 160
+        ev = det.push_tick(pcm[k * 1600:(k + 1) * 1600])
+        if ev is not None and not ev.skipped:
+            cm, cs = mfcc_ref.extract_mfcc(ev.audio)
+            mfcc_ref.similarity_from_stats(tm, ts, cm, cs)
+        ticks += 1
+    wall = time.perf_counter() - t0
+    return ticks, wall
+
+
+def cpu_stream_baseline(seconds, procs):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs, initializer=_pool_init) as pool:
+        res = pool.map(_cpu_stream_worker, [(9000 + p, seconds) for p in range(procs)])
+    rtf = sum(t * 0.1 / w for t, w in res)       # seconds of audio per second, summed over processes
+    return {"value": rtf, "unit": "streams sustained in real time", "cores": procs, "kind": "port",
+            "sample": f"{procs} processes x ~{seconds:.0f} s, each one synthetic stream of the streaming recipe "
+                      f"through oracle/gate_ref.py DetectorRef (ring, block RMS, pct25, FSM, cut) + "
+                      f"oracle/mfcc_ref.py level 2 per emitted segment, OMP_NUM_THREADS=1"}
+
+
 def _pool_init():
     os.environ["OMP_NUM_THREADS"] = "1"
     sys.path.insert(0, ROOT)
 
 
 # --------------------------------------------------------------------------- streaming (config 3)
-def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word):
+def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1, first_stream=0, cdev=None):
     """Full level-1 + level-2 engine on `n_streams` synthetic streams: 10 s
-    prefill, then `n_ticks` ticks launched one at a time (the real-time cadence)."""
+    prefill, then `n_ticks` ticks launched one at a time (the real-time cadence).
+    With world > 1 every tick also gathers the ranks' positive detections
+    {stream, tick, length, score} to rank 0 over RCCL (easywakeword_amd.shard.gather_positives)."""
     period_ticks = 160                       # 16 s loop per stream, distinct per stream
     P = period_ticks * 1600
     g = torch.Generator(device=dev)
@@ -185,6 +228,9 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word):
     base = pcm.data_ptr()
 
     events = []
+    gathered = [0]
+    if world > 1:
+        from easywakeword_amd.shard import gather_positives
 
     def run(t0, nt, per_call):
         t = t0
@@ -192,7 +238,16 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word):
             k = t % period_ticks
             n = min(per_call, nt - (t - t0), period_ticks - k)
             se.push_device(base + k * 1600 * 4, stride, 1600, n)
-            events.append(se.poll())        # the host consumes detections every call (callbacks)
+            ev = se.poll()                  # the host consumes detections every call (callbacks)
+            events.append(ev)
+            if world > 1:                   # positives of every rank -> rank 0 (level-3 input)
+                pos = ev[(ev["match"] != 0) & ((ev["flags"] & 1) == 0)]
+                rec = np.stack([pos["stream"].astype(np.int64) + first_stream, pos["tick"].astype(np.int64),
+                                pos["length"].astype(np.int64), pos["score"].view(np.int64)], axis=1) \
+                    if len(pos) else np.zeros((0, 4), np.int64)
+                out, _ = gather_positives(torch.from_numpy(rec).to(cdev))
+                if out is not None:
+                    gathered[0] += int(out.shape[0])
             t += n
         return t
 
@@ -219,6 +274,8 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word):
            "scorer_kernel_ms_per_tick": (sc_ms + r_ms) / max(1, sc_n),
            "events": int(len(real)), "matches": int(real["match"].sum()) if len(real) else 0,
            "mfcc_frames": int((1 + real["length"].astype(np.int64) // HOP).sum()) if len(real) else 0}
+    if world > 1:
+        out["positives_gathered_to_rank0"] = gathered[0]
     se.close()
     del pcm
     return out
@@ -235,10 +292,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    # EWK_BENCH_BACKEND=gloo rehearses the N>1 path with several ranks on one GPU
+    # (collectives on CPU copies); the real multi-GPU run uses RCCL ("nccl").
+    backend = os.environ.get("EWK_BENCH_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    cdev = dev if backend == "nccl" else torch.device("cpu")   # where collective buffers live
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import easywakeword_amd as ewa
     word = load_word()
@@ -256,13 +321,13 @@ def main():
     assert sh != 0
     if world > 1:
         from easywakeword_amd.shard import DecisionGather
-        gather = DecisionGather(score, match)   # tests/test_dist_gloo.py runs the same code over gloo
+        gather = DecisionGather(score.to(cdev), match.to(cdev))   # tests/test_dist_gloo.py: same code over gloo
 
     def step():
         eng.score_device(pcm.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n_seg, mean.data_ptr(),
                          std.data_ptr(), score.data_ptr(), match.data_ptr(), sh)
         if world > 1:   # gather every rank's decisions to all (rank 0 runs the confirm stage)
-            gather(score, match)
+            gather(score.to(cdev), match.to(cdev))
 
     torch.cuda.synchronize()
     for _ in range(args.warmup):
@@ -288,7 +353,7 @@ def main():
     r_ms, r_n = eng.profile_read(1)
     eng.profile(False)
     step_ms = ev0.elapsed_time(ev1) / args.steps
-    t_rank = torch.tensor([wall], dtype=torch.float64, device=dev)
+    t_rank = torch.tensor([wall], dtype=torch.float64, device=cdev)
     if world > 1:
         dist.all_reduce(t_rank, op=dist.ReduceOp.MAX)
     t_max = float(t_rank.item())
@@ -351,12 +416,16 @@ def main():
         sample = min(n_seg, 16 * 400)
         host = pcm[: int(offsets[sample - 1] + lengths[sample - 1])].cpu().numpy()
         out["cpu_baseline"] = cpu_baseline(host, lengths[:sample], offsets[:sample], args.cpu_seconds)
+        if not args.no_streaming:
+            out["cpu_baseline"]["streaming"] = cpu_stream_baseline(min(args.cpu_seconds, 10.0),
+                                                                   out["cpu_baseline"]["cores"])
     if not args.no_streaming:
         del pcm
         torch.cuda.empty_cache()
-        st = streaming_bench(torch, dev, ewa, args.stream_count, args.stream_ticks, args.seed + rank, word)
+        st = streaming_bench(torch, dev, ewa, args.stream_count, args.stream_ticks, args.seed + rank, word,
+                             world=world, first_stream=rank * args.stream_count, cdev=cdev)
         out["streaming"] = st
-        tot = torch.tensor([st["streams_realtime"]], dtype=torch.float64, device=dev)
+        tot = torch.tensor([st["streams_realtime"]], dtype=torch.float64, device=cdev)
         if world > 1:
             dist.all_reduce(tot)
         out["streams_realtime_total"] = float(tot.item())

@@ -48,6 +48,65 @@ class DecisionGather:
         return torch.cat(self.score_parts), torch.cat(self.match_parts)
 
 
+def gather_positives(records, audio=None, group=None, dst: int = 0):
+    """Gather every rank's positive detections to rank `dst`.
+
+    records: [n, k] int64 tensor on this rank, k >= 3 with column 2 = segment length
+             (the event fields: stream, tick, length, score bits, ...);
+    audio:   optional list of n 1-D float tensors (the segments' PCM, lengths as in column 2).
+    Collectives: an all_gather of the per-rank counts (and PCM totals), an all_gather
+    of the count-padded records, then point-to-point sends of each rank's packed PCM
+    to `dst` (batch_isend_irecv).  Returns (records, audio list) on `dst`, (None, None)
+    elsewhere.  The tensors must live where the backend expects them (CUDA for RCCL,
+    CPU for gloo).
+    """
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    n = records.shape[0]
+    k = records.shape[1] if records.dim() == 2 else 0
+    flat = torch.cat([a.reshape(-1) for a in audio]) if audio else None
+    total = 0 if flat is None else flat.numel()
+    meta = torch.tensor([n, total], dtype=torch.int64, device=records.device)
+    metas = [torch.empty_like(meta) for _ in range(world)]
+    dist.all_gather(metas, meta, group=group)
+    counts = [int(m[0]) for m in metas]
+    totals = [int(m[1]) for m in metas]
+    cap = max(1, max(counts))
+    padded = records.new_zeros((cap, k))
+    if n:
+        padded[:n] = records
+    parts = [torch.empty_like(padded) for _ in range(world)]
+    dist.all_gather(parts, padded, group=group)
+    out_rec = torch.cat([parts[r][:counts[r]] for r in range(world)]) if rank == dst else None
+    out_audio = None
+    if audio is not None:
+        ops, bufs = [], {}
+        if rank == dst:
+            for r in range(world):
+                if r == dst or totals[r] == 0:
+                    continue
+                bufs[r] = torch.empty(totals[r], dtype=flat.dtype if flat is not None else torch.float32,
+                                      device=records.device)
+                ops.append(dist.P2POp(dist.irecv, bufs[r], r, group=group))
+            if flat is not None:
+                bufs[dst] = flat
+        elif total:
+            ops.append(dist.P2POp(dist.isend, flat, dst, group=group))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        if rank == dst:
+            out_audio = []
+            for r in range(world):
+                lens = [int(x) for x in parts[r][:counts[r], 2]] if counts[r] else []
+                buf, o = bufs.get(r), 0
+                for ln in lens:
+                    out_audio.append(buf[o:o + ln])
+                    o += ln
+    return out_rec, out_audio
+
+
 def positives(scores, matches, first_stream_of_rank, segments_per_stream: int):
     """Global (stream, segment) ids of the gathered matches -- what rank 0 hands to the confirm stage."""
     import torch

@@ -14,7 +14,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from easywakeword_amd.shard import DecisionGather, positives, shard_streams
+from easywakeword_amd.shard import DecisionGather, gather_positives, positives, shard_streams
 
 N_STREAMS = 5
 SEG_PER_STREAM = 3
@@ -109,3 +109,50 @@ def test_gloo_world2_gather_matches_single_process():
         np.testing.assert_array_equal(m, ref_m)
         want = [(i // SEG_PER_STREAM, i % SEG_PER_STREAM) for i in np.nonzero(ref_m)[0]]
         assert [(a, b) for a, b, _ in pos] == want
+
+
+def _rank_positives(rank):
+    """Rank-dependent positives: rank 0 has 2, rank 1 has 3, rank 2 none (ragged, incl. empty)."""
+    n = [2, 3, 0][rank]
+    g = torch.Generator().manual_seed(10 + rank)
+    rec, audio = [], []
+    for i in range(n):
+        ln = 1000 + 137 * i + 50 * rank
+        rec.append([rank * 100 + i, 7 + i, ln, i])
+        audio.append(torch.randn(ln, generator=g))
+    return torch.tensor(rec, dtype=torch.int64).reshape(n, 4), audio
+
+
+def _worker_pos(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rec, audio = _rank_positives(rank)
+        out_rec, out_audio = gather_positives(rec, audio)
+        q.put((rank, None if out_rec is None else out_rec.numpy(),
+               None if out_audio is None else [a.numpy() for a in out_audio]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world3_gather_positives_with_pcm():
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_pos, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {r: (rec, aud) for r, rec, aud in [q.get(timeout=300) for _ in range(world)]}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want_rec = np.concatenate([_rank_positives(r)[0].numpy() for r in range(world)])
+    want_aud = [a.numpy() for r in range(world) for a in _rank_positives(r)[1]]
+    rec, aud = results[0]
+    np.testing.assert_array_equal(rec, want_rec)
+    assert len(aud) == len(want_aud) == 5
+    for a, b in zip(aud, want_aud):
+        np.testing.assert_array_equal(a, b)
+    assert results[1] == (None, None) and results[2] == (None, None)
