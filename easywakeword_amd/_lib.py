@@ -25,6 +25,8 @@ EWK_ENODEV = -5
 EWK_EV_SKIPPED = 1
 EWK_EV_RESCORED = 2
 EWK_PUSH_DEVICE = 1
+EWK_PCM_DEVICE = 1
+EWK_OUT_DEVICE = 4
 EWK_SCORE_REQUIRE_TEMPLATE = 1
 EWK_SCORE_F32_CANDIDATES = 2
 
@@ -37,6 +39,8 @@ EXPORTS = [
     "ewk_push", "ewk_push_many", "ewk_poll", "ewk_get_stream_state", "ewk_read_last",
     "ewk_read_segment", "ewk_reset_streams", "ewk_set_similarity_threshold",
     "ewk_profile_enable", "ewk_profile_read",
+    "ewk_push_pcm16", "ewk_push_many_pcm16", "ewk_normalize_segments", "ewk_normalize_events",
+    "ewk_decode_pcm16",
 ]
 
 
@@ -120,6 +124,11 @@ def load():
             "ewk_reset_streams": (C.c_int, [_P]),
             "ewk_profile_enable": (C.c_int, [_P, C.c_int32]),
             "ewk_profile_read": (C.c_int, [_P, C.c_int32, _dp, _i64p]),
+            "ewk_push_pcm16": (C.c_int, [_P, _P, C.c_int64, C.c_int32]),
+            "ewk_push_many_pcm16": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.c_int32, C.c_int32]),
+            "ewk_normalize_segments": (C.c_int, [_P, _P, C.c_int64, _i64p, _i32p, C.c_int32, _P, C.c_int32]),
+            "ewk_normalize_events": (C.c_int, [_P, C.POINTER(EwkEvent), C.c_int32, _P, C.c_int32]),
+            "ewk_decode_pcm16": (C.c_int, [_P, _P, C.c_int64, _P, C.c_int32]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)

@@ -51,6 +51,12 @@ struct DevBuf {
     }
 };
 
+// Scoped temporary device buffer (freed on return; callers synchronize before).
+template <typename T>
+struct TmpBuf : DevBuf<T> {
+    ~TmpBuf() { this->release(); }
+};
+
 }  // namespace
 
 struct ewk_engine {
@@ -619,16 +625,18 @@ static int score_pending(ewk_engine* e) {
     return EWK_OK;
 }
 
-static int push_impl(ewk_engine* e, const float* pcm, int64_t stride, int64_t tick_stride, int32_t n_ticks,
-                     int32_t flags) {
+static int push_impl(ewk_engine* e, const void* pcm_any, int64_t stride, int64_t tick_stride, int32_t n_ticks,
+                     int32_t flags, bool pcm16) {
     if (!e) return fail(EWK_EINVAL, "engine is NULL");
     if (e->n_streams <= 0) return fail(EWK_EINVAL, "engine has no streams");
-    if (!pcm) return fail(EWK_EINVAL, "pcm is NULL");
+    if (!pcm_any) return fail(EWK_EINVAL, "pcm is NULL");
     if (n_ticks <= 0) return fail(EWK_EINVAL, "n_ticks must be positive");
+    const size_t es = pcm16 ? sizeof(int16_t) : sizeof(float);
+    const unsigned char* pcm = static_cast<const unsigned char*>(pcm_any);
     if (stride < e->cfg.block && e->n_streams > 1) return fail(EWK_EINVAL, "stride must be >= block");
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = e->stream;
-    const float* src = pcm;
+    const void* src = pcm_any;
     int64_t st_stride = stride, tk_stride = tick_stride;
     if (!(flags & EWK_PUSH_DEVICE)) {
         // Gather the caller's (pageable) blocks into pinned staging on the CPU, then
@@ -640,16 +648,16 @@ static int push_impl(ewk_engine* e, const float* pcm, int64_t stride, int64_t ti
             if (e->h_stage) HIP_TRY(hipHostFree(e->h_stage));
             e->h_stage = nullptr;
             e->h_stage_cap = 0;
-            HIP_TRY(hipHostMalloc((void**)&e->h_stage, total * sizeof(float), hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc((void**)&e->h_stage, total * sizeof(float), hipHostMallocDefault));   // >= es bytes each
             e->h_stage_cap = total;
         }
         if (!e->h_stage_free) HIP_TRY(hipEventCreateWithFlags(&e->h_stage_free, hipEventDisableTiming));
         for (int32_t st = 0; st < e->n_streams; ++st)
             for (int32_t t = 0; t < n_ticks; ++t)
-                memcpy(e->h_stage + (size_t)st * per_stream + (size_t)t * e->cfg.block,
-                       pcm + (size_t)st * stride + (size_t)t * tick_stride, e->cfg.block * sizeof(float));
+                memcpy(reinterpret_cast<unsigned char*>(e->h_stage) + ((size_t)st * per_stream + (size_t)t * e->cfg.block) * es,
+                       pcm + ((size_t)st * stride + (size_t)t * tick_stride) * es, e->cfg.block * es);
         HIP_TRY(e->push_stage.reserve(total));
-        HIP_TRY(hipMemcpyAsync(e->push_stage.p, e->h_stage, total * sizeof(float), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(e->push_stage.p, e->h_stage, total * es, hipMemcpyHostToDevice, s));
         HIP_TRY(hipEventRecord(e->h_stage_free, s));
         src = e->push_stage.p;
         st_stride = (int64_t)per_stream;
@@ -660,7 +668,8 @@ static int push_impl(ewk_engine* e, const float* pcm, int64_t stride, int64_t ti
         const int32_t nt = std::min<int32_t>(32, n_ticks - t0);
         GateArgs g;
         memset(&g, 0, sizeof(g));
-        g.pcm = src + (int64_t)t0 * tk_stride;
+        if (pcm16) g.pcm16 = static_cast<const int16_t*>(src) + (int64_t)t0 * tk_stride;
+        else g.pcm = static_cast<const float*>(src) + (int64_t)t0 * tk_stride;
         g.stride = st_stride;
         g.tick_stride = tk_stride;
         g.n_ticks = nt;
@@ -702,12 +711,127 @@ static int push_impl(ewk_engine* e, const float* pcm, int64_t stride, int64_t ti
 }
 
 int ewk_push(ewk_engine* e, const float* pcm, int64_t stride, int32_t flags) {
-    return push_impl(e, pcm, stride, 0, 1, flags);
+    return push_impl(e, pcm, stride, 0, 1, flags, false);
 }
 
 int ewk_push_many(ewk_engine* e, const float* pcm, int64_t stride, int64_t tick_stride, int32_t n_ticks,
                   int32_t flags) {
-    return push_impl(e, pcm, stride, tick_stride, n_ticks, flags);
+    return push_impl(e, pcm, stride, tick_stride, n_ticks, flags, false);
+}
+
+int ewk_push_pcm16(ewk_engine* e, const int16_t* pcm, int64_t stride, int32_t flags) {
+    return push_impl(e, pcm, stride, 0, 1, flags, true);
+}
+
+int ewk_push_many_pcm16(ewk_engine* e, const int16_t* pcm, int64_t stride, int64_t tick_stride, int32_t n_ticks,
+                        int32_t flags) {
+    return push_impl(e, pcm, stride, tick_stride, n_ticks, flags, true);
+}
+
+// ---------------------------------------------------------------- level-3 input / PCM16 decode
+static int normalize_impl(ewk_engine* e, const float* d_pcm, const int64_t* offsets, const int32_t* lengths,
+                          const ewk_event* events, int32_t n, double* out, int32_t flags) {
+    hipStream_t s = e->stream;
+    std::vector<int64_t> oo(n);
+    int64_t total = 0;
+    for (int32_t i = 0; i < n; ++i) {
+        const int32_t len = events ? events[i].length : lengths[i];
+        if (len < 0) return fail(EWK_EINVAL, "negative segment length");
+        oo[i] = total;
+        total += len;
+    }
+    TmpBuf<int64_t> d_oo, d_off;
+    TmpBuf<int32_t> d_len;
+    TmpBuf<ewk_event> d_ev;
+    TmpBuf<double> d_out;
+    HIP_TRY(d_oo.reserve(std::max<int32_t>(1, n)));
+    HIP_TRY(hipMemcpyAsync(d_oo.p, oo.data(), n * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    L3Args a;
+    memset(&a, 0, sizeof(a));
+    a.n = n;
+    a.out_offsets = d_oo.p;
+    if (events) {
+        HIP_TRY(d_ev.reserve(std::max<int32_t>(1, n)));
+        HIP_TRY(hipMemcpyAsync(d_ev.p, events, n * sizeof(ewk_event), hipMemcpyHostToDevice, s));
+        a.events = d_ev.p;
+        a.pcm = e->d_ring;
+        a.ring_len = e->ring_len;
+    } else {
+        HIP_TRY(d_off.reserve(std::max<int32_t>(1, n)));
+        HIP_TRY(d_len.reserve(std::max<int32_t>(1, n)));
+        HIP_TRY(hipMemcpyAsync(d_off.p, offsets, n * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(d_len.p, lengths, n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        a.pcm = d_pcm;
+        a.offsets = d_off.p;
+        a.lengths = d_len.p;
+    }
+    if (flags & EWK_OUT_DEVICE) {
+        a.out = out;
+    } else {
+        HIP_TRY(d_out.reserve(std::max<int64_t>(1, total)));
+        a.out = d_out.p;
+    }
+    HIP_TRY(launch_normalize(a, s));
+    if (!(flags & EWK_OUT_DEVICE) && total > 0)
+        HIP_TRY(hipMemcpyAsync(out, d_out.p, total * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return EWK_OK;
+}
+
+int ewk_normalize_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int64_t* offsets,
+                           const int32_t* lengths, int32_t n_seg, double* out, int32_t flags) {
+    if (!e) return fail(EWK_EINVAL, "engine is NULL");
+    if (n_seg < 0 || n_pcm < 0) return fail(EWK_EINVAL, "negative size");
+    if (n_seg == 0) return EWK_OK;
+    if (!pcm || !offsets || !lengths || !out) return fail(EWK_EINVAL, "NULL argument");
+    for (int32_t i = 0; i < n_seg; ++i)
+        if (offsets[i] < 0 || lengths[i] < 0 || offsets[i] + lengths[i] > n_pcm)
+            return fail(EWK_EINVAL, "segment " + std::to_string(i) + " outside pcm");
+    HIP_TRY(hipSetDevice(e->device));
+    const float* d_pcm = pcm;
+    TmpBuf<float> tmp;
+    if (!(flags & EWK_PCM_DEVICE)) {
+        HIP_TRY(tmp.reserve(std::max<int64_t>(1, n_pcm)));
+        HIP_TRY(hipMemcpyAsync(tmp.p, pcm, n_pcm * sizeof(float), hipMemcpyHostToDevice, e->stream));
+        d_pcm = tmp.p;
+    }
+    return normalize_impl(e, d_pcm, offsets, lengths, nullptr, n_seg, out, flags);
+}
+
+int ewk_normalize_events(ewk_engine* e, const ewk_event* events, int32_t n, double* out, int32_t flags) {
+    if (!e) return fail(EWK_EINVAL, "engine is NULL");
+    if (n < 0) return fail(EWK_EINVAL, "negative size");
+    if (n == 0) return EWK_OK;
+    if (!events || !out) return fail(EWK_EINVAL, "NULL argument");
+    if (e->n_streams <= 0) return fail(EWK_EINVAL, "engine has no streams");
+    for (int32_t i = 0; i < n; ++i)
+        if (events[i].stream < 0 || events[i].stream >= e->n_streams || events[i].length < 0 ||
+            events[i].length > e->ring_len || events[i].ring_start < 0 || events[i].ring_start >= e->ring_len)
+            return fail(EWK_EINVAL, "event " + std::to_string(i) + " outside the rings");
+    HIP_TRY(hipSetDevice(e->device));
+    return normalize_impl(e, nullptr, nullptr, nullptr, events, n, out, flags);
+}
+
+int ewk_decode_pcm16(ewk_engine* e, const int16_t* in, int64_t n, float* out, int32_t flags) {
+    if (!e) return fail(EWK_EINVAL, "engine is NULL");
+    if (n < 0) return fail(EWK_EINVAL, "negative size");
+    if (n == 0) return EWK_OK;
+    if (!in || !out) return fail(EWK_EINVAL, "NULL argument");
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = e->stream;
+    if (flags & EWK_PCM_DEVICE) {   // both pointers device memory; asynchronous
+        HIP_TRY(launch_decode_pcm16(in, out, n, s));
+        return EWK_OK;
+    }
+    TmpBuf<int16_t> d_in;
+    TmpBuf<float> d_out;
+    HIP_TRY(d_in.reserve(n));
+    HIP_TRY(d_out.reserve(n));
+    HIP_TRY(hipMemcpyAsync(d_in.p, in, n * sizeof(int16_t), hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_decode_pcm16(d_in.p, d_out.p, n, s));
+    HIP_TRY(hipMemcpyAsync(out, d_out.p, n * sizeof(float), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return EWK_OK;
 }
 
 int ewk_poll(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out) {

@@ -58,6 +58,7 @@ void build_pw_tree(int n, PwTree* t);
 
 struct GateArgs {
     const float* pcm;        // stream s, tick t: pcm[s*stride + t*tick_stride + i]
+    const int16_t* pcm16;    // or int16 PCM (same indexing), decoded as x / 32768 (exact)
     int64_t stride;
     int64_t tick_stride;
     int32_t n_ticks;

@@ -263,10 +263,12 @@ __global__ __launch_bounds__(256) void k_gate_ticks(GateArgs g) {
             st.reentries += 1;
         }
         // ---- a1: ingest `fs` samples at the write pointer (and stage them in LDS)
-        const float* src = g.pcm + (int64_t)s * g.stride + (int64_t)t * g.tick_stride;
+        const int64_t so = (int64_t)s * g.stride + (int64_t)t * g.tick_stride;
+        const float* src = g.pcm + so;
+        const int16_t* src16 = g.pcm16 + so;
         const int p0 = st.pointer;
         for (int i = lane; i < fs; i += 64) {
-            const float x = src[i];
+            const float x = g.pcm16 ? (float)src16[i] * (1.0f / 32768.0f) : src[i];
             int k = p0 + i;
             if (k >= R) k -= R;
             ring[k] = x;

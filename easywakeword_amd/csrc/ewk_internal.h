@@ -89,4 +89,19 @@ hipError_t launch_score_f64(const Tables64* d_tab64, const ScoreArgs& a, int rin
                             double* d_scratch, int64_t scratch_per_seg, int grid,
                             double* out_mean64, double* out_std64, hipStream_t s);
 
+// Level-3 pre-processing (ewk_level3.hip): segment i is pcm[offsets[i] ...][:lengths[i]]
+// (linear) or the ring slice of events[i] (ring_len > 0); output at out[out_offsets[i]].
+struct L3Args {
+    const float* pcm;
+    const int64_t* offsets;
+    const int32_t* lengths;
+    const ewk_event* events;
+    int64_t ring_len;            // 0 = linear
+    const int64_t* out_offsets;
+    double* out;
+    int32_t n;
+};
+hipError_t launch_normalize(const L3Args& a, hipStream_t s);
+hipError_t launch_decode_pcm16(const int16_t* in, float* out, int64_t n, hipStream_t s);
+
 }  // namespace ewk

@@ -157,6 +157,32 @@ class Engine:
                                                _lib.dptr(score), self._flags(False, f32)))
         return mean, std, score
 
+    def normalize(self, segments) -> list:
+        """Level-3 pre-processing of each segment on the GPU (wakeword.py:1019-1025):
+        float64, bit-identical to the reference's numpy (see include/ewk.h)."""
+        segs = [_f32(s) for s in segments]
+        n = len(segs)
+        if n == 0:
+            return []
+        lengths = np.array([len(s) for s in segs], dtype=np.int32)
+        offsets = np.zeros(n, dtype=np.int64)
+        offsets[1:] = np.cumsum(lengths[:-1], dtype=np.int64)
+        pcm = np.ascontiguousarray(np.concatenate(segs), dtype=np.float32)
+        out = np.zeros(max(1, int(lengths.sum())), np.float64)
+        check(self._lib.ewk_normalize_segments(self._h, pcm.ctypes.data_as(C.c_void_p), len(pcm),
+                                               _lib.i64ptr(offsets), _lib.i32ptr(lengths), n,
+                                               out.ctypes.data_as(C.c_void_p), 0))
+        return [out[o:o + l] for o, l in zip(offsets, lengths)]
+
+    def decode_pcm16(self, pcm16: np.ndarray) -> np.ndarray:
+        """int16 PCM -> float32 (x / 32768, librosa.load's value for 16 kHz PCM16) on the GPU."""
+        a = np.ascontiguousarray(pcm16, dtype=np.int16)
+        out = np.zeros(a.shape, np.float32)
+        if a.size:
+            check(self._lib.ewk_decode_pcm16(self._h, a.ctypes.data_as(C.c_void_p), a.size,
+                                             out.ctypes.data_as(C.c_void_p), 0))
+        return out
+
     def score_device(self, pcm_ptr: int, offsets_ptr: int, lengths_ptr: int, n: int, mean_ptr: int,
                      std_ptr: int, score_ptr: int, match_ptr: int, stream: int = 0,
                      f32_candidates: bool = False) -> None:
@@ -194,6 +220,29 @@ class StreamEngine(Engine):
         nt = a.shape[1] // self.block
         if nt:
             check(self._lib.ewk_push_many(self._h, a.ctypes.data_as(C.c_void_p), a.shape[1], self.block, nt, 0))
+
+    def push_pcm16(self, pcm16: np.ndarray) -> None:
+        """Ticks of int16 PCM [n_streams, n_ticks * block] (host), decoded on the device."""
+        a = np.ascontiguousarray(pcm16, dtype=np.int16)
+        if a.ndim != 2 or a.shape[0] != self.n_streams or a.shape[1] % self.block:
+            raise ValueError("pcm16 must be [n_streams, n_ticks*block]")
+        nt = a.shape[1] // self.block
+        if nt:
+            check(self._lib.ewk_push_many_pcm16(self._h, a.ctypes.data_as(C.c_void_p), a.shape[1], self.block,
+                                                nt, 0))
+
+    def normalize_events(self, events: np.ndarray) -> list:
+        """Level-3 pre-processing of polled events straight from the rings (float64 per event)."""
+        ev = np.ascontiguousarray(events, dtype=_lib.EVENT_DTYPE)
+        n = len(ev)
+        if n == 0:
+            return []
+        lengths = ev["length"].astype(np.int64)
+        out = np.zeros(max(1, int(lengths.sum())), np.float64)
+        check(self._lib.ewk_normalize_events(self._h, ev.ctypes.data_as(C.POINTER(_lib.EwkEvent)), n,
+                                             out.ctypes.data_as(C.c_void_p), 0))
+        offs = np.concatenate([[0], np.cumsum(lengths)[:-1]])
+        return [out[o:o + l] for o, l in zip(offs, lengths)]
 
     def push_device(self, ptr: int, stride: int, tick_stride: int = 0, n_ticks: int = 1) -> None:
         check(self._lib.ewk_push_many(self._h, C.c_void_p(ptr), int(stride), int(tick_stride), int(n_ticks),

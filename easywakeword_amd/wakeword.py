@@ -178,15 +178,12 @@ def _default_source(device):
                       "pass source=ArraySource(...) or WavSource(...)") from exc
 
 
-def normalize_for_transcription(audio_samples: np.ndarray) -> np.ndarray:
-    """_transcribe_audio's pre-processing (wakeword.py:1019-1025)."""
-    a = np.asarray(audio_samples, dtype=np.float64)
-    a = a - np.mean(a)
-    max_val = np.max(np.abs(a)) if a.size else 0.0
-    if max_val > 0:
-        a = a / max_val
-    a = a * 1.5
-    return np.clip(a, -1.0, 1.0)
+def normalize_for_transcription(audio_samples: np.ndarray, engine=None) -> np.ndarray:
+    """_transcribe_audio's pre-processing (wakeword.py:1019-1025) on the GPU:
+    x - mean, / max|.| if > 0, * 1.5, clip [-1, 1], float64 as numpy computes it."""
+    from .engine import Engine
+    eng = engine if engine is not None else Engine()
+    return eng.normalize([np.asarray(audio_samples)])[0]
 
 
 class WakeWord:
@@ -403,7 +400,7 @@ class WakeWord:
         if self._confirm is None:
             return None
         try:
-            return self._confirm(normalize_for_transcription(audio_samples))
+            return self._confirm(normalize_for_transcription(audio_samples, self._sound_buffer.engine))
         except Exception as e:  # noqa: BLE001 - reference swallows (wakeword.py:1032-1034)
             self._log(f"Transcription failed: {e}", logging.ERROR)
             return None

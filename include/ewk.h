@@ -50,6 +50,8 @@ extern "C" {
 
 /* ewk_push flags */
 #define EWK_PUSH_DEVICE 1     /* pcm is a device pointer */
+#define EWK_PCM_DEVICE 1      /* input sample pointers are device memory (same bit as EWK_PUSH_DEVICE) */
+#define EWK_OUT_DEVICE 4      /* output pointer is device memory (asynchronous where noted) */
 
 typedef struct ewk_engine ewk_engine;
 
@@ -159,6 +161,11 @@ int ewk_push(ewk_engine* e, const float* pcm, int64_t stride, int32_t flags);
  * pcm[s*stride + t*tick_stride ...]. One launch sequence, no host sync. */
 int ewk_push_many(ewk_engine* e, const float* pcm, int64_t stride, int64_t tick_stride,
                   int32_t n_ticks, int32_t flags);
+/* int16 PCM variants (PortAudio / WAV PCM16 as delivered; decoded on the device as
+ * x / 32768 -- exactly soundfile's / librosa.load's float32 -- halving ingest bytes). */
+int ewk_push_pcm16(ewk_engine* e, const int16_t* pcm, int64_t stride, int32_t flags);
+int ewk_push_many_pcm16(ewk_engine* e, const int16_t* pcm, int64_t stride, int64_t tick_stride,
+                        int32_t n_ticks, int32_t flags);
 /* Drain up to `cap` queued events (blocks on the engine stream). */
 int ewk_poll(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out);
 int ewk_get_stream_state(ewk_engine* e, int32_t stream, ewk_stream_state* out);
@@ -168,6 +175,22 @@ int ewk_read_last(ewk_engine* e, int32_t stream, int64_t n_samples, float* out, 
 int ewk_read_segment(ewk_engine* e, int32_t stream, int64_t ring_start, int32_t length, float* out);
 /* Reset all stream state (ring, threshold, FSM, event queue). */
 int ewk_reset_streams(ewk_engine* e);
+
+/* ---- either side of the path --------------------------------------- */
+/* Level-3 input: WakeWord._transcribe_audio's normalisation (wakeword.py:1019-1025)
+ * y = x - mean(x); y /= max|y| if > 0; y *= 1.5; clip to [-1, 1], float64 and
+ * bit-identical to numpy (pairwise mean), on the device.  Outputs are packed:
+ * segment i starts at out[sum of the previous lengths].  out is host memory unless
+ * flags has EWK_OUT_DEVICE.  Segments of a float32 batch (pcm host memory unless
+ * EWK_PCM_DEVICE) ... */
+int ewk_normalize_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int64_t* offsets,
+                           const int32_t* lengths, int32_t n_seg, double* out, int32_t flags);
+/* ... or gated segments straight from the stream rings (polled events: stream,
+ * ring_start, length), the reference's word_audio of each event. */
+int ewk_normalize_events(ewk_engine* e, const ewk_event* events, int32_t n, double* out, int32_t flags);
+/* WAV / PCM16 ingest (librosa.load of a 16 kHz PCM16 file = int16 / 32768 as float32):
+ * host arrays unless EWK_PCM_DEVICE (then both are device memory, asynchronous). */
+int ewk_decode_pcm16(ewk_engine* e, const int16_t* in, int64_t n, float* out, int32_t flags);
 
 /* ---- measurement ------------------------------------------------------------ */
 /* When enabled, every scorer / gate launch is bracketed by hipEvents on the

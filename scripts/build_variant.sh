@@ -6,12 +6,12 @@ R="$(cd "$(dirname "$0")/.." && pwd)"
 REV=$1; NAME=$2; shift 2
 T=$(mktemp -d)
 mkdir -p "$T/easywakeword_amd/csrc" "$T/include" "$R/variants"
-for f in easywakeword_amd/csrc/ewk_mfcc.hip easywakeword_amd/csrc/ewk_gate.hip easywakeword_amd/csrc/ewk_engine.cpp \
+for f in easywakeword_amd/csrc/ewk_mfcc.hip easywakeword_amd/csrc/ewk_gate.hip easywakeword_amd/csrc/ewk_level3.hip easywakeword_amd/csrc/ewk_engine.cpp \
          easywakeword_amd/csrc/ewk_tables.cpp easywakeword_amd/csrc/ewk_internal.h easywakeword_amd/csrc/ewk_gate.h include/ewk.h; do
   if [ "$REV" = "WT" ]; then cp "$R/$f" "$T/$f"; else git -C "$R" show "$REV:$f" > "$T/$f"; fi
 done
 objs=""
-for s in ewk_mfcc.hip ewk_gate.hip ewk_engine.cpp ewk_tables.cpp; do
+for s in ewk_mfcc.hip ewk_gate.hip ewk_level3.hip ewk_engine.cpp ewk_tables.cpp; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function "$@" \
      -c "$T/easywakeword_amd/csrc/$s" -o "$T/$s.o" &
   objs="$objs $T/$s.o"
