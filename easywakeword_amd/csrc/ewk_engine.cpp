@@ -51,6 +51,8 @@ struct DevBuf {
     }
 };
 
+constexpr int32_t kPollChunk = 1024;   // events copied speculatively with the counters
+
 // Scoped temporary device buffer (freed on return; callers synchronize before).
 template <typename T>
 struct TmpBuf : DevBuf<T> {
@@ -104,6 +106,7 @@ struct ewk_engine {
     int32_t ev_cap = 0;
     DevBuf<float> push_stage;
     float* h_stage = nullptr;       // pinned host staging for ewk_push / ewk_push_many
+    unsigned char* h_poll = nullptr;   // pinned: event counters + the first kPollChunk events
     size_t h_stage_cap = 0;
     hipEvent_t h_stage_free = nullptr;   // recorded after the last DMA out of h_stage
     int64_t tick = 0;
@@ -230,6 +233,7 @@ void ewk_destroy(ewk_engine* e) {
     (void)hipFree(e->d_events);
     (void)hipFree(e->d_evc);
     if (e->h_stage) (void)hipHostFree(e->h_stage);
+    if (e->h_poll) (void)hipHostFree(e->h_poll);
     if (e->h_stage_free) (void)hipEventDestroy(e->h_stage_free);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -294,6 +298,7 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
     if ((err = e->rescore_buf.reserve(1 + e->rescore_cap)) != hipSuccess) return bail(err, "rescore");
     e->d_rescore = e->rescore_buf.p;
     if ((err = hipMalloc(&e->d_work, 4 * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
+    if ((err = hipMemset(e->d_work, 0, 4 * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
     // fp64 scratch: log-mel + mfcc rows for the longest ring segment
     {
         const int64_t tmax = 1 + e->ring_len / HOP;
@@ -595,6 +600,7 @@ int ewk_reset_streams(ewk_engine* e) {
         x.last_silent = 1;
     }
     HIP_TRY(hipMemcpyAsync(e->d_st, st.data(), st.size() * sizeof(GateStream), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(e->d_work, 0, 4 * sizeof(int32_t), s));
     zero_event_state(e);
     HIP_TRY(hipStreamSynchronize(s));
     e->tick = 0;
@@ -611,7 +617,8 @@ static int score_pending(ewk_engine* e) {
     a.n_events = e->d_evc;
     a.ev_base = e->d_evc + 2;
     a.n_seg = e->ev_cap;
-    HIP_TRY(hipMemsetAsync(e->d_rescore, 0, sizeof(int32_t), e->stream));
+    a.work = e->d_work + 1;            // ring-mode counters (zeroed at create, re-armed by k_advance)
+    a.rescore_count = e->d_work + 2;
     {
         ProfScope ps(e, 0, e->stream);
         HIP_TRY(launch_score_f32(e->d_tab, a, 1, e->stream));
@@ -621,7 +628,7 @@ static int score_pending(ewk_engine* e) {
         ProfScope ps(e, 1, e->stream);
         HIP_TRY(launch_score_f64(e->d_tab64, a, 1, e->f64_scratch.p, per, e->f64_grid, nullptr, nullptr, e->stream));
     }
-    HIP_TRY(launch_advance_watermark(e->d_evc + 2, e->d_evc, e->stream));
+    HIP_TRY(launch_advance_watermark(e->d_evc + 2, e->d_evc, e->d_work + 1, e->d_work + 2, e->stream));
     return EWK_OK;
 }
 
@@ -839,22 +846,30 @@ int ewk_poll(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out) {
     *n_out = 0;
     if (e->n_streams <= 0) return EWK_OK;
     HIP_TRY(hipSetDevice(e->device));
-    int32_t cnt[4];
-    HIP_TRY(hipMemcpyAsync(cnt, e->d_evc, sizeof(cnt), hipMemcpyDeviceToHost, e->stream));
+    // counters and a speculative first chunk of events in one round trip
+    if (!e->h_poll) {
+        HIP_TRY(hipHostMalloc((void**)&e->h_poll, 16 + (size_t)kPollChunk * sizeof(ewk_event), hipHostMallocDefault));
+    }
+    int32_t* cnt = reinterpret_cast<int32_t*>(e->h_poll);
+    ewk_event* spec = reinterpret_cast<ewk_event*>(e->h_poll + 16);
+    const int32_t chunk = std::min<int32_t>(kPollChunk, e->ev_cap);
+    HIP_TRY(hipMemcpyAsync(cnt, e->d_evc, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipMemcpyAsync(spec, e->d_events, (size_t)chunk * sizeof(ewk_event), hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     int32_t n = std::min(cnt[0], e->ev_cap);
     if (cnt[1] > 0) return fail(EWK_ENOMEM, "event queue overflow: " + std::to_string(cnt[1]) + " events dropped");
-    n = std::min(n, std::max(0, cap));
+    if (n > std::max(0, cap)) return fail(EWK_EINVAL, "poll capacity smaller than the queued events");
     if (n > 0 && out) {
-        HIP_TRY(hipMemcpy(out, e->d_events, (size_t)n * sizeof(ewk_event), hipMemcpyDeviceToHost));
+        memcpy(out, spec, (size_t)std::min(n, chunk) * sizeof(ewk_event));
+        if (n > chunk)
+            HIP_TRY(hipMemcpy(out + chunk, e->d_events + chunk, (size_t)(n - chunk) * sizeof(ewk_event),
+                              hipMemcpyDeviceToHost));
         // order deterministically by (tick, stream)
         std::sort(out, out + n, [](const ewk_event& x, const ewk_event& y) {
             return x.tick != y.tick ? x.tick < y.tick : x.stream < y.stream;
         });
     }
-    if (n < std::min(cnt[0], e->ev_cap)) return fail(EWK_EINVAL, "poll capacity smaller than the queued events");
-    zero_event_state(e);
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    zero_event_state(e);   // stream-ordered before the next push; no host wait needed
     *n_out = n;
     return EWK_OK;
 }

@@ -77,8 +77,9 @@ struct ScoreArgs {
 };
 
 hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mode, hipStream_t s);
-// ring mode: *ev_base = *n_events after a scoring pass
-hipError_t launch_advance_watermark(int32_t* ev_base, const int32_t* n_events, hipStream_t s);
+// ring mode: *ev_base = *n_events after a scoring pass; zero the ring-mode work counter and re-score count
+hipError_t launch_advance_watermark(int32_t* ev_base, const int32_t* n_events, int32_t* work,
+                                    int32_t* rescore_count, hipStream_t s);
 constexpr int kScoreGridMax = 512;   // 2 workgroups x 256 CUs: one resident wave of the grid
 constexpr int kScoreGridRing = 256;  // ring-mode grid (device-side event count)
 int score_grid(int n_seg, int ring_mode);

@@ -906,10 +906,17 @@ __global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__
 #endif
 }
 
-__global__ void k_advance(int32_t* ev_base, const int32_t* n_events) { *ev_base = *n_events; }
+// Ring-mode epilogue: advance the scored-event watermark and re-arm the ring-mode
+// work counter and re-score count for the next tick (saves two memsets per tick).
+__global__ void k_advance(int32_t* ev_base, const int32_t* n_events, int32_t* work, int32_t* rescore_count) {
+    *ev_base = *n_events;
+    *work = 0;
+    *rescore_count = 0;
+}
 
-hipError_t launch_advance_watermark(int32_t* ev_base, const int32_t* n_events, hipStream_t s) {
-    hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, s, ev_base, n_events);
+hipError_t launch_advance_watermark(int32_t* ev_base, const int32_t* n_events, int32_t* work,
+                                    int32_t* rescore_count, hipStream_t s) {
+    hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, s, ev_base, n_events, work, rescore_count);
     return hipGetLastError();
 }
 
@@ -920,8 +927,10 @@ int score_grid(int n_seg, int ring_mode) {
 hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mode, hipStream_t s) {
     if (a.n_seg <= 0) return hipSuccess;
     const int grid = score_grid(a.n_seg, ring_mode);
-    hipError_t e = hipMemsetAsync(a.work, 0, sizeof(int32_t), s);
-    if (e != hipSuccess) return e;
+    if (!ring_mode) {   // ring mode: k_advance re-arms the counter after each tick
+        hipError_t e = hipMemsetAsync(a.work, 0, sizeof(int32_t), s);
+        if (e != hipSuccess) return e;
+    }
     if (ring_mode)
         hipLaunchKernelGGL(k_score_f32<1>, dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
     else

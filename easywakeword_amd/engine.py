@@ -251,11 +251,12 @@ class StreamEngine(Engine):
     def poll(self, cap: Optional[int] = None) -> np.ndarray:
         """Drain queued events as a structured array (see _lib.EVENT_DTYPE)."""
         cap = int(cap or max(4096, 4 * self.n_streams))
-        buf = (_lib.EwkEvent * cap)()
-        n = C.c_int32(0)
-        check(self._lib.ewk_poll(self._h, buf, cap, C.byref(n)))
-        arr = np.frombuffer(buf, dtype=_lib.EVENT_DTYPE, count=n.value).copy()
-        return arr
+        if getattr(self, "_poll_buf", None) is None or len(self._poll_buf) < cap:
+            self._poll_buf = np.zeros(cap, dtype=_lib.EVENT_DTYPE)   # reused: polled every tick
+            self._poll_n = C.c_int32(0)
+        check(self._lib.ewk_poll(self._h, self._poll_buf.ctypes.data_as(C.POINTER(_lib.EwkEvent)), cap,
+                                 C.byref(self._poll_n)))
+        return self._poll_buf[: self._poll_n.value].copy()
 
     def state(self, stream: int) -> dict:
         st = _lib.EwkStreamState()
