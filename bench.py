@@ -232,13 +232,14 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
     if world > 1:
         from easywakeword_amd.shard import gather_positives
 
-    def run(t0, nt, per_call):
+    def run(t0, nt, per_call, lagged=False):
         t = t0
         while t < t0 + nt:
             k = t % period_ticks
             n = min(per_call, nt - (t - t0), period_ticks - k)
             se.push_device(base + k * 1600 * 4, stride, 1600, n)
-            ev = se.poll()                  # the host consumes detections every call (callbacks)
+            # the host consumes detections every call; lagged: tick t-1's events while the GPU runs tick t
+            ev = se.poll(lagged=lagged)
             events.append(ev)
             if world > 1:                   # positives of every rank -> rank 0 (level-3 input)
                 pos = ev[(ev["match"] != 0) & ((ev["flags"] & 1) == 0)]
@@ -257,7 +258,8 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
     se.profile(True)
     torch.cuda.synchronize()
     w0 = time.perf_counter()
-    t = run(t, n_ticks, 1)                   # one tick per call: the real-time cadence
+    t = run(t, n_ticks, 1, lagged=True)      # one tick per call: the real-time cadence, pipelined
+    events.append(se.poll())                 # the last tick's events
     se.sync()
     wall = time.perf_counter() - w0
     gate_ms, gate_n = se.profile_read(2)

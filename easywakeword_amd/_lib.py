@@ -40,7 +40,7 @@ EXPORTS = [
     "ewk_read_segment", "ewk_reset_streams", "ewk_set_similarity_threshold",
     "ewk_profile_enable", "ewk_profile_read",
     "ewk_push_pcm16", "ewk_push_many_pcm16", "ewk_normalize_segments", "ewk_normalize_events",
-    "ewk_decode_pcm16",
+    "ewk_decode_pcm16", "ewk_poll_lagged",
 ]
 
 
@@ -118,6 +118,7 @@ def load():
             "ewk_push": (C.c_int, [_P, _P, C.c_int64, C.c_int32]),
             "ewk_push_many": (C.c_int, [_P, _P, C.c_int64, C.c_int64, C.c_int32, C.c_int32]),
             "ewk_poll": (C.c_int, [_P, C.POINTER(EwkEvent), C.c_int32, _i32p]),
+            "ewk_poll_lagged": (C.c_int, [_P, C.POINTER(EwkEvent), C.c_int32, _i32p]),
             "ewk_get_stream_state": (C.c_int, [_P, C.c_int32, C.POINTER(EwkStreamState)]),
             "ewk_read_last": (C.c_int, [_P, C.c_int32, C.c_int64, _fp, _i64p]),
             "ewk_read_segment": (C.c_int, [_P, C.c_int32, C.c_int64, C.c_int32, _fp]),

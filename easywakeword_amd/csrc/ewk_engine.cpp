@@ -101,9 +101,18 @@ struct ewk_engine {
     double* d_sorted = nullptr;     // [streams][2][n_blocks] sorted block RMS (double-buffered)
     PwTree* d_trees = nullptr;      // numpy pairwise-sum trees for the block and the last 0.1 s
     GateStream* d_st = nullptr;
-    ewk_event* d_events = nullptr;
-    int32_t* d_evc = nullptr;   // [0] count, [1] dropped, [2] scored watermark
+    // Two event banks (ev_cap events + 4 counters each: [0] count, [1] dropped,
+    // [2] scored watermark): pushes append to `bank`; ewk_poll_lagged drains the
+    // other bank while the GPU still works on this one.
+    ewk_event* d_events = nullptr;   // [2][ev_cap]
+    int32_t* d_evc = nullptr;        // [2][4]
     int32_t ev_cap = 0;
+    int bank = 0;
+    bool bank_used[2] = {false, false};
+    hipEvent_t bank_done[2] = {nullptr, nullptr};   // recorded after the last push into a bank
+    hipStream_t cstream = nullptr;                  // D2H copies of drained banks
+    ewk_event* ev_bank(int b) { return d_events + (size_t)b * ev_cap; }
+    int32_t* evc_bank(int b) { return d_evc + 4 * b; }
     DevBuf<float> push_stage;
     float* h_stage = nullptr;       // pinned host staging for ewk_push / ewk_push_many
     unsigned char* h_poll = nullptr;   // pinned: event counters + the first kPollChunk events
@@ -149,7 +158,8 @@ struct ProfScope {
 };
 
 static void zero_event_state(ewk_engine* e) {
-    if (e->d_evc) (void)hipMemsetAsync(e->d_evc, 0, 4 * sizeof(int32_t), e->stream);
+    if (e->d_evc) (void)hipMemsetAsync(e->d_evc, 0, 8 * sizeof(int32_t), e->stream);
+    e->bank_used[0] = e->bank_used[1] = false;
 }
 
 // The re-score list holds at most one entry per segment of a launch.
@@ -236,6 +246,9 @@ void ewk_destroy(ewk_engine* e) {
     if (e->h_poll) (void)hipHostFree(e->h_poll);
     if (e->h_stage_free) (void)hipEventDestroy(e->h_stage_free);
     if (e->stream) (void)hipStreamDestroy(e->stream);
+    if (e->cstream) (void)hipStreamDestroy(e->cstream);
+    for (int b = 0; b < 2; ++b)
+        if (e->bank_done[b]) (void)hipEventDestroy(e->bank_done[b]);
     delete e;
 }
 
@@ -277,6 +290,10 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
     };
     hipError_t err;
     if ((err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking)) != hipSuccess) return bail(err, "stream");
+    if ((err = hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking)) != hipSuccess) return bail(err, "stream");
+    for (int b = 0; b < 2; ++b)
+        if ((err = hipEventCreateWithFlags(&e->bank_done[b], hipEventDisableTiming)) != hipSuccess)
+            return bail(err, "event");
     {
         std::vector<unsigned char> buf(sizeof(Tables));
         Tables* t = reinterpret_cast<Tables*>(buf.data());
@@ -330,9 +347,9 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
         e->ev_cap = std::max(4096, 4 * n_streams);
         if ((err = reserve_rescore(e, e->ev_cap)) != hipSuccess) return bail(err, "rescore list");
         if ((err = reserve_lm(e, e->ev_cap, 1)) != hipSuccess) return bail(err, "log-mel scratch");
-        if ((err = hipMalloc(&e->d_events, (size_t)e->ev_cap * sizeof(ewk_event))) != hipSuccess)
+        if ((err = hipMalloc(&e->d_events, 2 * (size_t)e->ev_cap * sizeof(ewk_event))) != hipSuccess)
             return bail(err, "events");
-        if ((err = hipMalloc(&e->d_evc, 4 * sizeof(int32_t))) != hipSuccess) return bail(err, "event counters");
+        if ((err = hipMalloc(&e->d_evc, 8 * sizeof(int32_t))) != hipSuccess) return bail(err, "event counters");
         e->gate_stage = gate_stage_len(c.block, e->n_last);
         int rc = ewk_reset_streams(e);
         if (rc != EWK_OK) {
@@ -613,9 +630,9 @@ static int score_pending(ewk_engine* e) {
     ScoreArgs a = base_args(e);
     a.pcm = e->d_ring;
     a.ring_len = e->ring_len;
-    a.events = e->d_events;
-    a.n_events = e->d_evc;
-    a.ev_base = e->d_evc + 2;
+    a.events = e->ev_bank(e->bank);
+    a.n_events = e->evc_bank(e->bank);
+    a.ev_base = e->evc_bank(e->bank) + 2;
     a.n_seg = e->ev_cap;
     a.work = e->d_work + 1;            // ring-mode counters (zeroed at create, re-armed by k_advance)
     a.rescore_count = e->d_work + 2;
@@ -628,7 +645,8 @@ static int score_pending(ewk_engine* e) {
         ProfScope ps(e, 1, e->stream);
         HIP_TRY(launch_score_f64(e->d_tab64, a, 1, e->f64_scratch.p, per, e->f64_grid, nullptr, nullptr, e->stream));
     }
-    HIP_TRY(launch_advance_watermark(e->d_evc + 2, e->d_evc, e->d_work + 1, e->d_work + 2, e->stream));
+    HIP_TRY(launch_advance_watermark(e->evc_bank(e->bank) + 2, e->evc_bank(e->bank), e->d_work + 1, e->d_work + 2,
+                                     e->stream));
     return EWK_OK;
 }
 
@@ -702,9 +720,9 @@ static int push_impl(ewk_engine* e, const void* pcm_any, int64_t stride, int64_t
         g.max_segment_seconds = e->cfg.max_segment_seconds;
         g.reentry_timeout = e->cfg.reentry_timeout;
         g.min_threshold = e->cfg.min_threshold;
-        g.events = e->d_events;
-        g.ev_count = e->d_evc;
-        g.ev_dropped = e->d_evc + 1;
+        g.events = e->ev_bank(e->bank);
+        g.ev_count = e->evc_bank(e->bank);
+        g.ev_dropped = e->evc_bank(e->bank) + 1;
         g.ev_cap = e->ev_cap;
         {
             ProfScope ps(e, 2, s);
@@ -714,6 +732,8 @@ static int push_impl(ewk_engine* e, const void* pcm_any, int64_t stride, int64_t
         int rc = score_pending(e);
         if (rc) return rc;
     }
+    HIP_TRY(hipEventRecord(e->bank_done[e->bank], s));
+    e->bank_used[e->bank] = true;
     return EWK_OK;
 }
 
@@ -841,36 +861,71 @@ int ewk_decode_pcm16(ewk_engine* e, const int16_t* in, int64_t n, float* out, in
     return EWK_OK;
 }
 
-int ewk_poll(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out) {
-    if (!e || !n_out) return fail(EWK_EINVAL, "NULL argument");
+// Copy out one bank's events once the pushes into it have completed (copy stream,
+// no wait on later work), then re-arm its counters on the engine stream.
+static int drain_bank(ewk_engine* e, int b, ewk_event* out, int32_t cap, int32_t* n_out) {
     *n_out = 0;
-    if (e->n_streams <= 0) return EWK_OK;
-    HIP_TRY(hipSetDevice(e->device));
-    // counters and a speculative first chunk of events in one round trip
-    if (!e->h_poll) {
+    if (!e->bank_used[b]) return EWK_OK;
+    if (!e->h_poll)
         HIP_TRY(hipHostMalloc((void**)&e->h_poll, 16 + (size_t)kPollChunk * sizeof(ewk_event), hipHostMallocDefault));
-    }
     int32_t* cnt = reinterpret_cast<int32_t*>(e->h_poll);
     ewk_event* spec = reinterpret_cast<ewk_event*>(e->h_poll + 16);
     const int32_t chunk = std::min<int32_t>(kPollChunk, e->ev_cap);
-    HIP_TRY(hipMemcpyAsync(cnt, e->d_evc, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipMemcpyAsync(spec, e->d_events, (size_t)chunk * sizeof(ewk_event), hipMemcpyDeviceToHost, e->stream));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(hipStreamWaitEvent(e->cstream, e->bank_done[b], 0));
+    HIP_TRY(hipMemcpyAsync(cnt, e->evc_bank(b), 4 * sizeof(int32_t), hipMemcpyDeviceToHost, e->cstream));
+    HIP_TRY(hipMemcpyAsync(spec, e->ev_bank(b), (size_t)chunk * sizeof(ewk_event), hipMemcpyDeviceToHost,
+                           e->cstream));
+    HIP_TRY(hipStreamSynchronize(e->cstream));
     int32_t n = std::min(cnt[0], e->ev_cap);
     if (cnt[1] > 0) return fail(EWK_ENOMEM, "event queue overflow: " + std::to_string(cnt[1]) + " events dropped");
     if (n > std::max(0, cap)) return fail(EWK_EINVAL, "poll capacity smaller than the queued events");
     if (n > 0 && out) {
         memcpy(out, spec, (size_t)std::min(n, chunk) * sizeof(ewk_event));
-        if (n > chunk)
-            HIP_TRY(hipMemcpy(out + chunk, e->d_events + chunk, (size_t)(n - chunk) * sizeof(ewk_event),
-                              hipMemcpyDeviceToHost));
-        // order deterministically by (tick, stream)
-        std::sort(out, out + n, [](const ewk_event& x, const ewk_event& y) {
-            return x.tick != y.tick ? x.tick < y.tick : x.stream < y.stream;
-        });
+        if (n > chunk) {
+            HIP_TRY(hipMemcpyAsync(out + chunk, e->ev_bank(b) + chunk, (size_t)(n - chunk) * sizeof(ewk_event),
+                                   hipMemcpyDeviceToHost, e->cstream));
+            HIP_TRY(hipStreamSynchronize(e->cstream));
+        }
     }
-    zero_event_state(e);   // stream-ordered before the next push; no host wait needed
+    // re-arm: stream-ordered before any later push into this bank
+    HIP_TRY(hipMemsetAsync(e->evc_bank(b), 0, 4 * sizeof(int32_t), e->stream));
+    e->bank_used[b] = false;
     *n_out = n;
+    return EWK_OK;
+}
+
+static void sort_events(ewk_event* out, int32_t n) {   // deterministic order: (tick, stream)
+    std::sort(out, out + n, [](const ewk_event& x, const ewk_event& y) {
+        return x.tick != y.tick ? x.tick < y.tick : x.stream < y.stream;
+    });
+}
+
+int ewk_poll(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out) {
+    if (!e || !n_out) return fail(EWK_EINVAL, "NULL argument");
+    *n_out = 0;
+    if (e->n_streams <= 0) return EWK_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    int32_t n0 = 0, n1 = 0;
+    const int older = e->bank ^ 1;
+    int rc = drain_bank(e, older, out, cap, &n0);
+    if (rc) return rc;
+    rc = drain_bank(e, e->bank, out ? out + n0 : nullptr, cap - n0, &n1);
+    if (rc) return rc;
+    if (out) sort_events(out, n0 + n1);
+    *n_out = n0 + n1;
+    return EWK_OK;
+}
+
+int ewk_poll_lagged(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out) {
+    if (!e || !n_out) return fail(EWK_EINVAL, "NULL argument");
+    *n_out = 0;
+    if (e->n_streams <= 0) return EWK_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    const int older = e->bank ^ 1;
+    int rc = drain_bank(e, older, out, cap, n_out);
+    if (rc) return rc;
+    if (out) sort_events(out, *n_out);
+    e->bank = older;   // later pushes append to the drained bank; the newest one drains next time
     return EWK_OK;
 }
 

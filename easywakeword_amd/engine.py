@@ -248,14 +248,16 @@ class StreamEngine(Engine):
         check(self._lib.ewk_push_many(self._h, C.c_void_p(ptr), int(stride), int(tick_stride), int(n_ticks),
                                       _lib.EWK_PUSH_DEVICE))
 
-    def poll(self, cap: Optional[int] = None) -> np.ndarray:
-        """Drain queued events as a structured array (see _lib.EVENT_DTYPE)."""
+    def poll(self, cap: Optional[int] = None, lagged: bool = False) -> np.ndarray:
+        """Drain queued events as a structured array (see _lib.EVENT_DTYPE).
+        lagged=True: the events of the pushes before the previous lagged poll, without
+        waiting for the latest push (pipelined serving; see include/ewk.h)."""
         cap = int(cap or max(4096, 4 * self.n_streams))
         if getattr(self, "_poll_buf", None) is None or len(self._poll_buf) < cap:
             self._poll_buf = np.zeros(cap, dtype=_lib.EVENT_DTYPE)   # reused: polled every tick
             self._poll_n = C.c_int32(0)
-        check(self._lib.ewk_poll(self._h, self._poll_buf.ctypes.data_as(C.POINTER(_lib.EwkEvent)), cap,
-                                 C.byref(self._poll_n)))
+        fn = self._lib.ewk_poll_lagged if lagged else self._lib.ewk_poll
+        check(fn(self._h, self._poll_buf.ctypes.data_as(C.POINTER(_lib.EwkEvent)), cap, C.byref(self._poll_n)))
         return self._poll_buf[: self._poll_n.value].copy()
 
     def state(self, stream: int) -> dict:

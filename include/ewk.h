@@ -166,8 +166,12 @@ int ewk_push_many(ewk_engine* e, const float* pcm, int64_t stride, int64_t tick_
 int ewk_push_pcm16(ewk_engine* e, const int16_t* pcm, int64_t stride, int32_t flags);
 int ewk_push_many_pcm16(ewk_engine* e, const int16_t* pcm, int64_t stride, int64_t tick_stride,
                         int32_t n_ticks, int32_t flags);
-/* Drain up to `cap` queued events (blocks on the engine stream). */
+/* Drain up to `cap` queued events (waits for every push so far). */
 int ewk_poll(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out);
+/* Pipelined drain: returns the events of the pushes made before the previous
+ * ewk_poll_lagged call, without waiting for the pushes made since -- the GPU
+ * keeps working on tick t while the host consumes tick t-1 (one call of latency). */
+int ewk_poll_lagged(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out);
 int ewk_get_stream_state(ewk_engine* e, int32_t stream, ewk_stream_state* out);
 /* SoundBuffer.return_last_n_seconds(n) (wakeword.py:498-513) as float32 (ring values are the float32 input). */
 int ewk_read_last(ewk_engine* e, int32_t stream, int64_t n_samples, float* out, int64_t* n_out);

@@ -128,3 +128,29 @@ def test_unaligned_block_512_thresholds():
         if det.started and det.buf.is_buffer_full():
             assert bool(st["last_silent"]) == det.buf.is_silent(), k
             assert st["state"] == det.state, k
+
+
+def test_lagged_poll_pipelines_one_call_behind():
+    """ewk_poll_lagged returns exactly the events a blocking poll returns, one push call later."""
+    from easywakeword_amd import StreamEngine
+    parts = [synth.make_stream(seed, n_words=4)[0] for seed in (31, 32, 33, 34)]
+    n = min(len(p) for p in parts) // 1600 * 1600
+    pcm = np.stack([p[:n] for p in parts]).astype(np.float32)
+    word = synth.load_word()
+    a, b = StreamEngine(4), StreamEngine(4)
+    for e in (a, b):
+        e.template_from_pcm(word)
+    blocking, lagged = [], []
+    for t0 in range(0, n // 1600, 4):
+        blk = pcm[:, t0 * 1600:(t0 + 4) * 1600]
+        if blk.shape[1] < 4 * 1600:
+            break
+        a.push_many(blk)
+        blocking.append(a.poll())
+        b.push_many(blk)
+        lagged.append(b.poll(lagged=True))
+    lagged.append(b.poll())          # drain the last call
+    assert len(lagged[0]) == 0
+    for k, ev in enumerate(blocking):
+        np.testing.assert_array_equal(lagged[k + 1], ev)
+    assert sum(len(e) for e in blocking) >= 8
