@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--no-streaming", action="store_true")
     ap.add_argument("--stream-count", type=int, default=8192, help="config 3 streams per GPU")
     ap.add_argument("--stream-ticks", type=int, default=600, help="ticks after the 10 s prefill")
+    ap.add_argument("--confirm-batch", type=int, default=64, help="config 5: Whisper-tiny batch (0 = skip)")
     return ap.parse_args()
 
 
@@ -199,7 +200,34 @@ def _pool_init():
 
 
 # --------------------------------------------------------------------------- streaming (config 3)
-def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1, first_stream=0, cdev=None):
+def confirm_bench(se, ev, final_tick, batch, dev):
+    """Level 3: GPU normalisation of gathered positives straight from the
+    rings (bit-exact wakeword.py:1019-1025), then one batched Whisper-tiny decode."""
+    import torch
+    from easywakeword_amd.confirm import WhisperConfirm
+    pos = ev[(ev["match"] != 0) & ((ev["flags"] & 1) == 0) & (ev["tick"] > final_tick - 80)]
+    pos = pos[np.argsort(-pos["tick"], kind="stable")][:batch]
+    if len(pos) == 0:
+        return {"segments": 0}
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    audio = se.normalize_events(pos)
+    t1 = time.perf_counter()
+    wc = WhisperConfirm(device=dev)
+    wc.transcribe(audio[:2])                        # warm-up (kernels, allocator)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    wc.transcribe(audio)
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    return {"segments": int(len(pos)), "normalize_ms": (t1 - t0) * 1e3, "whisper_batch_ms": (t3 - t2) * 1e3,
+            "segments_per_s": len(pos) / (t3 - t2 + t1 - t0), "max_new_tokens": wc.max_new_tokens,
+            "model": "whisper-tiny dims (transformers WhisperConfig default), random init: no weights offline "
+                     "(timing only, parity unpinned)"}
+
+
+def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1, first_stream=0, cdev=None,
+                    confirm_batch=0):
     """Full level-1 + level-2 engine on `n_streams` synthetic streams: 10 s
     prefill, then `n_ticks` ticks launched one at a time (the real-time cadence).
     With world > 1 every tick also gathers the ranks' positive detections
@@ -278,6 +306,8 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
            "mfcc_frames": int((1 + real["length"].astype(np.int64) // HOP).sum()) if len(real) else 0}
     if world > 1:
         out["positives_gathered_to_rank0"] = gathered[0]
+    if confirm_batch > 0:   # config 5: level 3 on the latest positives still in the rings
+        out["confirm"] = confirm_bench(se, ev, t, confirm_batch, dev)
     se.close()
     del pcm
     return out
@@ -425,7 +455,8 @@ def main():
         del pcm
         torch.cuda.empty_cache()
         st = streaming_bench(torch, dev, ewa, args.stream_count, args.stream_ticks, args.seed + rank, word,
-                             world=world, first_stream=rank * args.stream_count, cdev=cdev)
+                             world=world, first_stream=rank * args.stream_count, cdev=cdev,
+                             confirm_batch=args.confirm_batch if rank == 0 else 0)
         out["streaming"] = st
         tot = torch.tensor([st["streams_realtime"]], dtype=torch.float64, device=cdev)
         if world > 1:
