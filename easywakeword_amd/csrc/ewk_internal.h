@@ -19,7 +19,19 @@ constexpr int NMFCC = EWK_N_MFCC;    // 20
 constexpr int MEL_ITERS = 40;        // unrolled mel FMAs per lane: sum of per-group band widths
 constexpr int DCT_PITCH = 130;       // LDS row pitch of the DCT table (bank-conflict free A reads)
 constexpr int SCR_FRAME = 272;       // per-frame FFT scratch floats (16 rows x 17)
-constexpr int WAVES = 4;             // waves per workgroup in the fp32 scorer
+// fp32 scorer shape: frames per 16-lane group per pass (kNF), waves per workgroup and
+// workgroups per CU.  kNF = 2 doubles the per-wave FFT state (ILP) and its LDS, so the
+// CU holds one 8-wave workgroup instead of two 4-wave ones (same 2 waves per SIMD).
+#ifndef EWK_NF
+#define EWK_NF 2
+#endif
+constexpr int kNF = EWK_NF;
+// kNF = 2: the untangle pairs conjugate bins inside a lane (two columns of one frame)
+#ifndef EWK_PAIR
+#define EWK_PAIR (EWK_NF == 2)
+#endif
+constexpr int WAVES = kNF == 1 ? 4 : 8;
+constexpr int kScoreWGsPerCU = kNF == 1 ? 2 : 1;
 
 // Host-built constant tables (ewk_tables.cpp); copied to LDS by every workgroup.
 struct Tables {
@@ -80,8 +92,8 @@ hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mo
 // ring mode: *ev_base = *n_events after a scoring pass; zero the ring-mode work counter and re-score count
 hipError_t launch_advance_watermark(int32_t* ev_base, const int32_t* n_events, int32_t* work,
                                     int32_t* rescore_count, hipStream_t s);
-constexpr int kScoreGridMax = 512;   // 2 workgroups x 256 CUs: one resident wave of the grid
-constexpr int kScoreGridRing = 256;  // ring-mode grid (device-side event count)
+constexpr int kScoreGridMax = 256 * kScoreWGsPerCU;   // one resident workgroup wave of the grid
+constexpr int kScoreGridRing = 256;                     // ring-mode grid (device-side event count)
 int score_grid(int n_seg, int ring_mode);
 // log-mel tiles parked per wave for the top_db pass: segments up to 3 s (T <= 301)
 constexpr int kLmTiles = (1 + 48000 / HOP + 15) / 16;

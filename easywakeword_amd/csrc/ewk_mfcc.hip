@@ -72,16 +72,22 @@ constexpr int L_WPAD = L_TW2 + 16 * TP * 8;               // [j][kMelOff[i] + q]
 constexpr int L_BLO = L_WPAD + 16 * WP * 4;
 constexpr int L_DCT = L_BLO + NMEL * 4;
 constexpr int L_SHARED_END = ((L_DCT + NMFCC * DCT_PITCH * 4) + 15) & ~15;
-constexpr int W_SCR = 0;                                  // 4 frames x 272 floats (also the sample staging)
-constexpr int W_TILE = W_SCR + 4 * SCR_FRAME * 4;         // 16 x 128 floats, XOR-swizzled rows
+// Frames per wave pass: kNF per 16-lane group (kNF = 2: two independent FFTs per lane).
+constexpr int kFPP = 4 * kNF;
+constexpr int kStageLoads = ((kFPP - 1) * HOP + NFFT + 63) / 64;   // dword loads per lane per pass
+// frame fr's FFT scratch starts at fr * 272 + 8 * (fr >> 2): the two frames a 16-lane
+// group untangles side by side (fr, fr + 4) land 8 banks apart
+constexpr int kScrFrames = kFPP * SCR_FRAME + 8 * (kNF - 1);
+constexpr int kScrFloats = (kScrFrames > 64 * kStageLoads) ? kScrFrames : 64 * kStageLoads;
+constexpr int W_SCR = 0;                                  // kFPP frames x 272 floats (also the sample staging)
+constexpr int W_TILE = W_SCR + kScrFloats * 4;            // 16 x 128 floats, XOR-swizzled rows
 constexpr int W_MISC = W_SCR;                             // 64 floats, aliases the FFT scratch (epilogue only)
 constexpr int W_TMIN = W_TILE + 16 * NMEL * 4;            // per-tile log-mel minima (kLmTiles floats)
 constexpr int W_BYTES = W_TMIN + ((kLmTiles * 4 + 15) & ~15);
 constexpr int LDS_BYTES = L_SHARED_END + WAVES * W_BYTES;
 constexpr int kRescoreFrames = 16;
-constexpr int kStage = 1024;                              // staged samples per pass (>= 3*160 + 512)
-static_assert(LDS_BYTES <= 80 * 1024, "two workgroups per CU must fit");
-static_assert(kStage <= 4 * SCR_FRAME, "staging must fit the FFT scratch");
+static_assert(LDS_BYTES * kScoreWGsPerCU <= 160 * 1024, "the workgroups of a CU must fit its LDS");
+static_assert(16 % kFPP == 0, "passes must tile the 16-frame log-mel tile");
 
 
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
@@ -159,11 +165,11 @@ __device__ __forceinline__ SegSrc<RING> make_src(const float* p, int64_t start, 
     return v;
 }
 
-// Coalesced staging loads: lane l fetches samples q0 + 64*c + l, c = 0..15.
+// Coalesced staging loads: lane l fetches samples q0 + 64*c + l, c < kStageLoads.
 template <int RING>
-__device__ __forceinline__ void stage_load(const SegSrc<RING>& v, int q0, int lane, float (&r)[16]) {
+__device__ __forceinline__ void stage_load(const SegSrc<RING>& v, int q0, int lane, float (&r)[kStageLoads]) {
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
+    for (int c = 0; c < kStageLoads; ++c) {
         const int q = q0 + 64 * c + lane;
 #if EWK_ABLATE & 1
         r[c] = ((unsigned)q < (unsigned)v.len) ? (float)((q * 7) & 255) * 1e-3f : 0.0f;
@@ -180,9 +186,9 @@ __device__ __forceinline__ void stage_load(const SegSrc<RING>& v, int q0, int la
     }
 }
 
-__device__ __forceinline__ void stage_store(float* stage, int lane, const float (&r)[16]) {
+__device__ __forceinline__ void stage_store(float* stage, int lane, const float (&r)[kStageLoads]) {
 #pragma unroll
-    for (int c = 0; c < 16; ++c) stage[64 * c + lane] = r[c];
+    for (int c = 0; c < kStageLoads; ++c) stage[64 * c + lane] = r[c];
 }
 
 constexpr int kMelW[8] = {2, 2, 2, 3, 4, 6, 9, 12};   // per 16-band group (checked on the host)
@@ -204,84 +210,141 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
                                            int lane, const int (&lo)[8], float& vmax, float& vmin,
                                            uint64_t* tim = nullptr) {
     EWK_TS(p0);
+    // lane group f = lane>>4 holds frames fr = 4 g + f (g < kNF) of this pass; the
+    // kNF frames of a lane are independent instruction streams (ILP for the wave).
     const int f = lane >> 4, j = lane & 15;
-    const int t = t0 + f;
-    const bool valid = t < T;
-    float* sc = scr + f * SCR_FRAME;
+#if EWK_PAIR
+    // after the transpose lane (h, j') = (j >> 3, j & 7) owns bin columns rowA = j' and
+    // rowB = 16 - j' (8 for j' = 0) of frame 4h + f (scratch scf)
+    const int jp = j & 7;
+    const int rowA = jp, rowB = jp ? 16 - jp : 8;
+    float* scf = scr + (4 * (j >> 3) + f) * SCR_FRAME + 8 * (j >> 3);
+#endif
+    bool valid[kNF];
+    float* sc[kNF];
+#pragma unroll
+    for (int g = 0; g < kNF; ++g) {
+        valid[g] = t0 + 4 * g + f < T;
+        sc[g] = scr + (4 * g + f) * SCR_FRAME + 8 * g;
+    }
 
     // ---- window the staged samples: lane j holds z[16*n1 + j] = x[32*n1+2j] + i x[32*n1+2j+1]
-    // (16 single ds_read_b64: the compiler would pair them into ds_read2_b64, which
+    // (single ds_read_b64s: the compiler would pair them into ds_read2_b64, which
     // costs the LDS twice the cycles per byte)
-    float2 a[16];
+    float2 a[kNF][16];
     {
-        const uint32_t sa = (uint32_t)(uintptr_t)(scr + f * HOP + 2 * j);
-        float2 x[16];
-#define EWK_LD64(n) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(x[n]) : "v"(sa), "i"(128 * (n)) : "memory")
-        EWK_LD64(0); EWK_LD64(1); EWK_LD64(2); EWK_LD64(3); EWK_LD64(4); EWK_LD64(5); EWK_LD64(6); EWK_LD64(7);
-        EWK_LD64(8); EWK_LD64(9); EWK_LD64(10); EWK_LD64(11); EWK_LD64(12); EWK_LD64(13); EWK_LD64(14); EWK_LD64(15);
+        float2 x[kNF][16];
+#pragma unroll
+        for (int g = 0; g < kNF; ++g) {
+            const uint32_t sa = (uint32_t)(uintptr_t)(scr + (4 * g + f) * HOP + 2 * j);
+#define EWK_LD64(n) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(x[g][n]) : "v"(sa), "i"(128 * (n)) : "memory")
+            EWK_LD64(0); EWK_LD64(1); EWK_LD64(2); EWK_LD64(3); EWK_LD64(4); EWK_LD64(5); EWK_LD64(6); EWK_LD64(7);
+            EWK_LD64(8); EWK_LD64(9); EWK_LD64(10); EWK_LD64(11); EWK_LD64(12); EWK_LD64(13); EWK_LD64(14); EWK_LD64(15);
 #undef EWK_LD64
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]), "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]),
-                       "+v"(x[8]), "+v"(x[9]), "+v"(x[10]), "+v"(x[11]), "+v"(x[12]), "+v"(x[13]), "+v"(x[14]),
-                       "+v"(x[15])
-                     :
-                     : "memory");
+        }
+#pragma unroll
+        for (int g = 0; g < kNF; ++g)
+            asm volatile("s_waitcnt lgkmcnt(0)"
+                         : "+v"(x[g][0]), "+v"(x[g][1]), "+v"(x[g][2]), "+v"(x[g][3]), "+v"(x[g][4]), "+v"(x[g][5]),
+                           "+v"(x[g][6]), "+v"(x[g][7]), "+v"(x[g][8]), "+v"(x[g][9]), "+v"(x[g][10]), "+v"(x[g][11]),
+                           "+v"(x[g][12]), "+v"(x[g][13]), "+v"(x[g][14]), "+v"(x[g][15])
+                         :
+                         : "memory");
         const float4* w4 = reinterpret_cast<const float4*>(smem + L_WIN2) + j * (TP / 2);
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             const float4 w = w4[c];
-            a[2 * c] = make_float2(x[2 * c].x * w.x, x[2 * c].y * w.y);
-            a[2 * c + 1] = make_float2(x[2 * c + 1].x * w.z, x[2 * c + 1].y * w.w);
+#pragma unroll
+            for (int g = 0; g < kNF; ++g) {
+                a[g][2 * c] = make_float2(x[g][2 * c].x * w.x, x[g][2 * c].y * w.y);
+                a[g][2 * c + 1] = make_float2(x[g][2 * c + 1].x * w.z, x[g][2 * c + 1].y * w.w);
+            }
         }
     }
     lds_order();
     EWK_TS(p1);
     if (tim) EWK_TACC(8, p0, p1);
-    // ---- prefetch the next pass while this one computes
-    float pf[16];
-    if (next) stage_load(v, (t0 + 4) * HOP - NFFT / 2, lane, pf);
+    // next pass's samples: issued before the mel stage (registers are free there),
+    // stored to the staging area at the end of the pass
+    float pf[kStageLoads];
     EWK_TS(p2);
     if (tim) EWK_TACC(9, p1, p2);
-    // ---- DFT16 over n1, twiddle W256^(j*k1)
-    dft16_perm(a);
+    // ---- DFT16 over n1, twiddle W256^(j*k1) (one twiddle row serves every frame of the lane)
+#pragma unroll
+    for (int g = 0; g < kNF; ++g) dft16_perm(a[g]);
     {
         const float4* t4 = reinterpret_cast<const float4*>(smem + L_TW1) + j * (TP / 2);
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             const float4 w = t4[c];   // k1 = 2c+1, 2c+2
-            a[dperm(2 * c + 1)] = cmul(a[dperm(2 * c + 1)], make_float2(w.x, w.y));
-            if (c < 7) a[dperm(2 * c + 2)] = cmul(a[dperm(2 * c + 2)], make_float2(w.z, w.w));
+#pragma unroll
+            for (int g = 0; g < kNF; ++g) {
+                a[g][dperm(2 * c + 1)] = cmul(a[g][dperm(2 * c + 1)], make_float2(w.x, w.y));
+                if (c < 7) a[g][dperm(2 * c + 2)] = cmul(a[g][dperm(2 * c + 2)], make_float2(w.z, w.w));
+            }
         }
     }
     EWK_TS(p3);
     if (tim) EWK_TACC(10, p2, p3);
     // ---- transpose through LDS (real, then imaginary half): lane k1 <- A_{n2}[k1].
     // Row r (16 floats) keeps column n in 4-float chunk (n>>2) ^ ((r>>2)&3): the
-    // column writes (ds_write_b32, frames f/f+1 272 floats apart) and the row reads
-    // (ds_read_b128) are both bank-conflict free.
-    float2 b[16];
+    // column writes (ds_write_b32, the frames of a 32-lane half 272 floats apart) and
+    // the row reads (ds_read_b128) are both bank-conflict free.
+    float2 b[kNF][16];
 #if EWK_ABLATE & 2
 #pragma unroll
-    for (int k1 = 0; k1 < 16; ++k1) b[k1] = a[dperm(k1)];
+    for (int g = 0; g < kNF; ++g)
+#pragma unroll
+        for (int k1 = 0; k1 < 16; ++k1) b[g][k1] = a[g][dperm(k1)];
 #else
     {
         const int jc = 4 * (j >> 2), jl = j & 3;
-        const float4* rd = reinterpret_cast<const float4*>(sc + 16 * j);
+#if !EWK_PAIR
         const int rsw = (j >> 2) & 3;
+#endif
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
 #pragma unroll
-            for (int k1 = 0; k1 < 16; ++k1) {
-                const float2 v = a[dperm(k1)];
-                sc[16 * k1 + (jc ^ (4 * ((k1 >> 2) & 3))) + jl] = half ? v.y : v.x;
-            }
-            lds_order();
+            for (int g = 0; g < kNF; ++g)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const float4 r = rd[c ^ rsw];
-                if (half) { b[4 * c].y = r.x; b[4 * c + 1].y = r.y; b[4 * c + 2].y = r.z; b[4 * c + 3].y = r.w; }
-                else      { b[4 * c].x = r.x; b[4 * c + 1].x = r.y; b[4 * c + 2].x = r.z; b[4 * c + 3].x = r.w; }
+                for (int k1 = 0; k1 < 16; ++k1) {
+                    const float2 vv = a[g][dperm(k1)];
+                    sc[g][16 * k1 + (jc ^ (4 * ((k1 >> 2) & 3))) + jl] = half ? vv.y : vv.x;
+                }
+            lds_order();
+#if EWK_PAIR
+            // lane (h, j') = (j >> 3, j & 7) reads two columns of frame 4h + f: c0 = j' and its
+            // conjugate partner 16 - j' (column 8 beside column 0 for j' = 0)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int r = s2 ? rowB : rowA;
+                const float4* rd = reinterpret_cast<const float4*>(scf + 16 * r);
+                const int rs = (r >> 2) & 3;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float4 q = rd[c ^ rs];
+                    if (half) {
+                        b[s2][4 * c].y = q.x; b[s2][4 * c + 1].y = q.y; b[s2][4 * c + 2].y = q.z; b[s2][4 * c + 3].y = q.w;
+                    } else {
+                        b[s2][4 * c].x = q.x; b[s2][4 * c + 1].x = q.y; b[s2][4 * c + 2].x = q.z; b[s2][4 * c + 3].x = q.w;
+                    }
+                }
             }
+#else
+#pragma unroll
+            for (int g = 0; g < kNF; ++g) {
+                const float4* rd = reinterpret_cast<const float4*>(sc[g] + 16 * j);
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float4 r = rd[c ^ rsw];
+                    if (half) {
+                        b[g][4 * c].y = r.x; b[g][4 * c + 1].y = r.y; b[g][4 * c + 2].y = r.z; b[g][4 * c + 3].y = r.w;
+                    } else {
+                        b[g][4 * c].x = r.x; b[g][4 * c + 1].x = r.y; b[g][4 * c + 2].x = r.z; b[g][4 * c + 3].x = r.w;
+                    }
+                }
+            }
+#endif
             lds_order();
         }
     }
@@ -289,9 +352,58 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     EWK_TS(p4);
     if (tim) EWK_TACC(11, p3, p4);
     // ---- DFT16 over n2: Z[j + 16*k2] = b[dperm(k2)]
-    dft16_perm(b);
+#pragma unroll
+    for (int g = 0; g < kNF; ++g) dft16_perm(b[g]);
     EWK_TS(p5);
     if (tim) EWK_TACC(12, p4, p5);
+#if EWK_PAIR
+    // ---- untangle + power, two conjugate bins per step, no cross-lane traffic.  For
+    // k = c0 + 16 it the partner Zp = Z[256 - k] sits in this lane's other column; with
+    // A = Z[k] + conj(Zp), B = Z[k] - conj(Zp), C = i W512^k B:
+    //   P'[k] = |2 X[k]|^2 = |A - C|^2,  P'[256 - k] = |A + C|^2.
+    // Lanes j' = 1..7: it = 0..15 (it = 16 repeats it = 15).  Lane j' = 0 pairs column
+    // 0 with itself (it = 0..8: k = 16 it, 256 - k; it = 0 yields bin 256) and column 8
+    // with itself (it = 9..16: k = 8 + 16 (it - 9)).
+    {
+        const bool z0 = jp == 0;
+        const float2* tw = reinterpret_cast<const float2*>(smem + L_TW2) + jp * TP;   // [j'][it], 17 entries
+        float* pA0 = scf + rowA;                     // P[k]      at pA0[16 it]       (it <= 15)
+        float* pA1 = z0 ? scf - 136 : pA0;           //           lane 0, it >= 9
+        float* pA2 = z0 ? scf - 136 : pA0 - 16;      //           it = 16
+        float* pB0 = scf - rowA;                     // P[256-k]  at pB0[256 - 16 it]
+        float* pB1 = z0 ? scf + 136 : pB0;
+        float* pB2 = z0 ? scf + 136 : pB0 + 16;
+#pragma unroll
+        for (int it = 0; it < 17; ++it) {
+            const float2 w = tw[it];   // (cos, sin)(2 pi k / 512)
+            const float2 ug = b[0][dperm(it < 16 ? it : 15)];
+            const float2 vg = b[1][dperm(it < 16 ? 15 - it : 0)];
+            float2 u, vv;
+            if (it <= 8) {
+                u = ug;
+                const float2 vz = b[0][dperm((16 - it) & 15)];
+                vv = z0 ? vz : vg;
+            } else {
+                const float2 uz = b[1][dperm(it - 9)], vz = b[1][dperm(24 - it)];
+                u = z0 ? uz : ug;
+                vv = z0 ? vz : vg;
+            }
+            const float ar = u.x + vv.x, ai = u.y - vv.y;
+            const float br = u.x - vv.x, bi = u.y + vv.y;
+            const float cr = w.y * br - w.x * bi;
+            const float ci = w.y * bi + w.x * br;
+            const float yr = ar - cr, yi = ai - ci;
+            const float xr = ar + cr, xi = ai + ci;
+            float* pa = it <= 8 ? pA0 : (it < 16 ? pA1 : pA2);
+            float* pb = it <= 8 ? pB0 : (it < 16 ? pB1 : pB2);
+            pa[16 * it] = yr * yr + yi * yi;
+            pb[256 - 16 * it] = xr * xr + xi * xi;
+        }
+        // the zero pad (bins 257..271) the unrolled band loops read past bin 256
+        scf[257 + jp] = 0.0f;
+        if (jp < 7) scf[265 + jp] = 0.0f;
+    }
+#else
     // ---- untangle + power, one bin column at a time.  Partner Z[(256-k) & 255] of
     // k = j + 16*k2 comes straight from the partner lane's registers: for j >= 1 it is
     // lane 16-j's slot 15-k2 (DPP row_mirror then row_shr:1); lane 0 keeps its own
@@ -305,76 +417,94 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
                 const int k2 = 2 * c + u;
-                const float2 src = b[dperm(15 - k2)], own = b[dperm((16 - k2) & 15)];
-                const int mx = __builtin_amdgcn_mov_dpp(__float_as_int(src.x), 0x140, 0xf, 0xf, false);   // row_mirror
-                const int my = __builtin_amdgcn_mov_dpp(__float_as_int(src.y), 0x140, 0xf, 0xf, false);
-                const float px = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.x), mx, 0x111, 0xf, 0xf, false));
-                const float py = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.y), my, 0x111, 0xf, 0xf, false));
                 const float2 cs = u ? make_float2(w.z, w.w) : make_float2(w.x, w.y);
-                const float2 z = b[dperm(k2)];
-                const float ar = z.x + px, ai = z.y - py;
-                const float br = z.x - px, bi = z.y + py;
-                const float yr = ar - cs.y * br + cs.x * bi;
-                const float yi = ai - cs.y * bi - cs.x * br;
-                sc[j + 16 * k2] = yr * yr + yi * yi;
+#pragma unroll
+                for (int g = 0; g < kNF; ++g) {
+                    const float2 src = b[g][dperm(15 - k2)], own = b[g][dperm((16 - k2) & 15)];
+                    const int mx = __builtin_amdgcn_mov_dpp(__float_as_int(src.x), 0x140, 0xf, 0xf, false);   // row_mirror
+                    const int my = __builtin_amdgcn_mov_dpp(__float_as_int(src.y), 0x140, 0xf, 0xf, false);
+                    const float px = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.x), mx, 0x111, 0xf, 0xf, false));
+                    const float py = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.y), my, 0x111, 0xf, 0xf, false));
+                    const float2 z = b[g][dperm(k2)];
+                    const float ar = z.x + px, ai = z.y - py;
+                    const float br = z.x - px, bi = z.y + py;
+                    const float yr = ar - cs.y * br + cs.x * bi;
+                    const float yi = ai - cs.y * bi - cs.x * br;
+                    sc[g][j + 16 * k2] = yr * yr + yi * yi;
+                }
             }
         }
     }
-    {   // bin 256 (X[256] = Re Z[0] - Im Z[0]) and the zero pad the unrolled band loops read past it
-        const float2 z0 = b[dperm(0)];
+#pragma unroll
+    for (int g = 0; g < kNF; ++g) {   // bin 256 (X[256] = Re Z[0] - Im Z[0]) and the zero pad the band loops read past it
+        const float2 z0 = b[g][dperm(0)];
         const float y = 2.0f * (z0.x - z0.y);
-        sc[256 + j] = (j == 0) ? y * y : 0.0f;
+        sc[g][256 + j] = (j == 0) ? y * y : 0.0f;
     }
+#endif
     lds_order();
     EWK_TS(p6);
     if (tim) EWK_TACC(13, p5, p6);
-    // ---- mel + log: lane j computes bands m = j + 16*i of its frame
-    float db[8];
+    if (next) stage_load(v, (t0 + kFPP) * HOP - NFFT / 2, lane, pf);
+    // ---- mel + log: lane j computes bands m = j + 16*i of its frames (weights shared).
+    // The stage's LDS reads go in two batches (band groups 0-5, then 6-7: 19 and 21
+    // weights), each followed by its FMAs -- one wait per batch, not one per group.
+    float db[kNF][8];
     {
         const float* wrow = reinterpret_cast<const float*>(smem + L_WPAD) + j * WP;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            float wv[12];
-            if (kMelW[i] <= 2) {
-                const float2 w = *reinterpret_cast<const float2*>(wrow + kMelOff[i]);
-                wv[0] = w.x; wv[1] = w.y;
-            } else {
+        for (int hh = 0; hh < 2; ++hh) {
+            const int i0 = hh ? 6 : 0, i1 = hh ? 8 : 6;
+            float wv[MEL_ITERS], pv[kNF][MEL_ITERS];
 #pragma unroll
-                for (int c = 0; c < (kMelW[i] + 3) / 4; ++c) {
-                    const float4 w = *reinterpret_cast<const float4*>(wrow + kMelOff[i] + 4 * c);
-                    wv[4 * c] = w.x; wv[4 * c + 1] = w.y; wv[4 * c + 2] = w.z; wv[4 * c + 3] = w.w;
+            for (int i = i0; i < i1; ++i) {
+                if (kMelW[i] <= 2) {
+                    const float2 w = *reinterpret_cast<const float2*>(wrow + kMelOff[i]);
+                    wv[kMelIt0[i]] = w.x; wv[kMelIt0[i] + 1] = w.y;
+                } else {
+#pragma unroll
+                    for (int c = 0; c < (kMelW[i] + 3) / 4; ++c) {
+                        const float4 w = *reinterpret_cast<const float4*>(wrow + kMelOff[i] + 4 * c);
+                        const float ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (4 * c + e < kMelW[i]) wv[kMelIt0[i] + 4 * c + e] = ww[e];
+                    }
+                }
+#pragma unroll
+                for (int g = 0; g < kNF; ++g) {
+                    const float* sp = sc[g] + lo[i];
+#pragma unroll
+                    for (int q = 0; q < kMelW[i]; ++q) pv[g][kMelIt0[i] + q] = sp[q];
                 }
             }
-            const float* sp = sc + lo[i];
-            float acc = 0.0f;
-#if EWK_ABLATE & 4
-            acc = wv[0] * sp[0] + 1.0f;
-#else
 #pragma unroll
-            for (int q = 0; q < kMelW[i]; ++q) acc = fmaf(wv[q], sp[q], acc);
-#endif
-#if EWK_ABLATE & 8
-            db[i] = acc;
-#else
-            // 10*log10(x) = (10*log10(2)) * log2(x), v_log_f32
-            db[i] = 3.0102999566398120f * __log2f(fmaxf(1e-10f, acc));
-#endif
+            for (int i = i0; i < i1; ++i)
+#pragma unroll
+                for (int g = 0; g < kNF; ++g) {
+                    float acc = 0.0f;
+#pragma unroll
+                    for (int q = 0; q < kMelW[i]; ++q) acc = fmaf(wv[kMelIt0[i] + q], pv[g][kMelIt0[i] + q], acc);
+                    // 10*log10(x) = (10*log10(2)) * log2(x), v_log_f32
+                    db[g][i] = 3.0102999566398120f * __log2f(fmaxf(1e-10f, acc));
+                }
         }
     }
     EWK_TS(p7);
     if (tim) EWK_TACC(14, p6, p7);
     lds_order();
-    {
-        const int r = row0 + f;
+#pragma unroll
+    for (int g = 0; g < kNF; ++g) {
+        const int r = row0 + 4 * g + f;
         const int sw = tile_swz(r);
         const int jx = j ^ (sw & 15), sb = sw >> 4;
         float* re = tile + r * NMEL + jx + 16 * sb;   // even i: column 16*(i+sb) + jx
         float* ro = tile + r * NMEL + jx - 16 * sb;   // odd  i: column 16*(i-sb) + jx
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            vmax = fmaxf(vmax, valid ? db[i] : -INFINITY);
-            vmin = fminf(vmin, valid ? db[i] : INFINITY);
-            ((i & 1) ? ro : re)[16 * i] = valid ? db[i] : 0.0f;
+            vmax = fmaxf(vmax, valid[g] ? db[g][i] : -INFINITY);
+            vmin = fminf(vmin, valid[g] ? db[g][i] : INFINITY);
+            ((i & 1) ? ro : re)[16 * i] = valid[g] ? db[g][i] : 0.0f;
         }
     }
     lds_order();
@@ -511,8 +641,9 @@ __device__ __forceinline__ void finish_stats(int T, const float (&cref)[8], doub
     }
 }
 
-__device__ __forceinline__ void zero_row(float* tile, int r, int lane) {
-    for (int m = lane & 15; m < NMEL; m += 16) tile[r * NMEL + m] = 0.0f;
+// Zero the kFPP tile rows of one pass (frames past T).
+__device__ __forceinline__ void zero_rows(float* tile, int row0, int lane) {
+    for (int m = lane; m < kFPP * NMEL; m += 64) tile[row0 * NMEL + m] = 0.0f;
 }
 
 // Whole segment for one wave.  gscr: this wave's log-mel scratch -- `scr_tiles` flat
@@ -525,7 +656,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     const int T = 1 + v.len / HOP;
     const int ntile = (T + 15) >> 4;
-    const int npass = (T + 3) >> 2;
+    const int npass = (T + kFPP - 1) / kFPP;
     const bool park = ntile <= scr_tiles;
     const int col = lane & 15;
     float4* gcol = gscr + (int64_t)scr_tiles * 8 * 64;
@@ -534,7 +665,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
     float vmax = -INFINITY, vmin = INFINITY;
     {   // stage the first pass synchronously
-        float r[16];
+        float r[kStageLoads];
         stage_load(v, -NFFT / 2, lane, r);
         stage_store(scr, lane, r);
         lds_order();
@@ -544,12 +675,12 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         float tmin = INFINITY;
         EWK_TS(t0);
 #pragma unroll 1
-        for (int p = 0; p < 4; ++p) {
-            const int pass = tile_i * 4 + p;
+        for (int p = 0; p < 16 / kFPP; ++p) {
+            const int pass = tile_i * (16 / kFPP) + p;
             if (pass < npass)
-                frame_pass(v, pass * 4, T, p * 4, pass + 1 < npass, smem, scr, tile, lane, lo, vmax, tmin, tim);
+                frame_pass(v, pass * kFPP, T, p * kFPP, pass + 1 < npass, smem, scr, tile, lane, lo, vmax, tmin, tim);
             else   // rows of frames past T: zero (ignored by the statistics)
-                zero_row(tile, p * 4 + (lane >> 4), lane);
+                zero_rows(tile, p * kFPP, lane);
         }
         lds_order();
         EWK_TS(t1);
@@ -622,7 +753,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
 #pragma unroll
             for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; }
             {
-                float r[16];
+                float r[kStageLoads];
                 stage_load(v, -NFFT / 2, lane, r);
                 stage_store(scr, lane, r);
                 lds_order();
@@ -630,12 +761,12 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
             float d0 = 0.f, d1 = 0.f;
             for (int tile_i = 0; tile_i < ntile; ++tile_i) {
 #pragma unroll 1
-                for (int p = 0; p < 4; ++p) {
-                    const int pass = tile_i * 4 + p;
+                for (int p = 0; p < 16 / kFPP; ++p) {
+                    const int pass = tile_i * (16 / kFPP) + p;
                     if (pass < npass)
-                        frame_pass(v, pass * 4, T, p * 4, pass + 1 < npass, smem, scr, tile, lane, lo, d0, d1);
+                        frame_pass(v, pass * kFPP, T, p * kFPP, pass + 1 < npass, smem, scr, tile, lane, lo, d0, d1);
                     else
-                        zero_row(tile, p * 4 + (lane >> 4), lane);
+                        zero_rows(tile, p * kFPP, lane);
                 }
                 lds_order();
 #pragma unroll
@@ -755,7 +886,7 @@ __device__ __forceinline__ double score_f32_finish(float uu_m, float uu_s, float
 }
 
 template <int RING>
-__global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__ tab, ScoreArgs a) {
+__global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const Tables* __restrict__ tab, ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // ---- cooperative table load (global -> LDS), per-lane rows transposed
     {
@@ -766,8 +897,18 @@ __global__ __launch_bounds__(256, 2) void k_score_f32(const Tables* __restrict__
             const int j = i & 15, n = i >> 4;   // win2[16n + j], tw1[16n + j], tw2[j + 16n]
             sw2[j * TP + n] = tab->win2[i];
             if (n > 0) st1[j * TP + n - 1] = tab->tw1[i];
+#if !EWK_PAIR
             st2[j * TP + n] = tab->tw2[i];
+#endif
         }
+#if EWK_PAIR
+        // [j'][it] = tw2[k] for the bin k that lane class j' untangles at step it
+        for (int i = threadIdx.x; i < 8 * 17; i += blockDim.x) {
+            const int jp = i / 17, it = i % 17;
+            const int k = jp ? jp + 16 * (it < 16 ? it : 15) : (it <= 8 ? 16 * it : 8 + 16 * (it - 9));
+            st2[jp * TP + it] = tab->tw2[k];
+        }
+#endif
         int* sb = reinterpret_cast<int*>(smem + L_BLO);
         for (int i = threadIdx.x; i < NMEL; i += blockDim.x) sb[i] = tab->band_lo[i];
         float* sw = reinterpret_cast<float*>(smem + L_WPAD);
