@@ -42,6 +42,7 @@ METRIC = "real-time 16 kHz streams sustained + MFCC frames/sec at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_FRAME = 640          # 160 new fp32 samples per MFCC frame
 HOP = 160
+SR = 16000
 
 
 def parse():
@@ -57,6 +58,8 @@ def parse():
     ap.add_argument("--no-streaming", action="store_true")
     ap.add_argument("--stream-count", type=int, default=8192, help="config 3 streams per GPU")
     ap.add_argument("--stream-ticks", type=int, default=600, help="ticks after the 10 s prefill")
+    ap.add_argument("--fixed-len", type=int, default=16000,
+                    help="also time the scorer on segments of this one length (0 = skip)")
     ap.add_argument("--confirm-batch", type=int, default=64, help="config 5: Whisper-tiny batch (0 = skip)")
     return ap.parse_args()
 
@@ -68,10 +71,13 @@ def load_word() -> np.ndarray:
     return np.frombuffer(raw, dtype="<i2").astype(np.float32) / np.float32(32768.0)
 
 
-def make_segments(torch, dev, n_seg, seed, word):
-    """Synthetic ragged batch on the GPU (deterministic per seed)."""
+def make_segments(torch, dev, n_seg, seed, word, fixed_len=0):
+    """Synthetic ragged batch on the GPU (deterministic per seed); fixed_len > 0: every
+    segment that many samples (SURVEY.md 8d config 2's L = 16000 / T = 101 variant)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     lengths = rng.integers(6400, 33600 + 1, n_seg).astype(np.int32)
+    if fixed_len > 0:
+        lengths[:] = fixed_len
     offsets = np.zeros(n_seg, np.int64)
     offsets[1:] = np.cumsum(lengths[:-1], dtype=np.int64)
     total = int(lengths.sum())
@@ -153,6 +159,25 @@ def cpu_baseline(host_pcm, lengths, offsets, seconds):
                       f"{procs} processes x ~{seconds:.0f} s, OMP_NUM_THREADS=1"}
 
 
+def event_sources(word, rng):
+    """[5, len(word)] float32 event sources of the streaming recipe:
+    the word, then distractors -- an 880 Hz tone burst and the time-reversed word (both
+    score above 75 against the word, false positives of the reference's matcher: MFCC
+    mean/std are time-symmetric and dominated by c0), a high-passed noise burst (scores
+    ~50-80) and a loud white-noise burst (negative similarity -> NaN score, no match)."""
+    wl = len(word)
+    tt = np.arange(wl, dtype=np.float64) / SR
+    peak = float(np.abs(word).max())
+    return np.stack([word, peak * 0.5 * np.sin(2 * np.pi * 880.0 * tt), word[::-1],
+                     np.diff(rng.standard_normal(wl + 1)) * 0.5,
+                     rng.standard_normal(wl) * 1.5]).astype(np.float32)
+
+
+def event_kind(rng, n):
+    """Per-event source index: the word with probability 1/2, else one of the four distractors."""
+    return np.where(rng.random(n) < 0.5, 0, rng.integers(1, 5, n))
+
+
 def _cpu_stream_worker(args):
     """Faithful CPU level 1 + level 2 (oracle/gate_ref.py DetectorRef + mfcc_ref scoring of every
     emitted segment) on one synthetic stream of the streaming bench's recipe, ~`seconds` of work."""
@@ -164,9 +189,10 @@ def _cpu_stream_worker(args):
     rng = np.random.Generator(np.random.PCG64(seed))
     P = 160 * 1600
     pcm = (rng.standard_normal(P) * rng.uniform(1e-4, 3e-3)).astype(np.float32)
+    table = event_sources(word, rng)
     for e in range(5):
         pos = e * P // 5 + int(rng.integers(0, 8000))
-        src = word[::-1] if rng.random() < 0.3 else word
+        src = table[int(event_kind(rng, 1)[0])]
         pcm[pos:pos + len(word)] += (src * rng.uniform(0.3, 2.0)).astype(np.float32)
     det = gate_ref.DetectorRef(gate_ref.GateConfig(), keep_audio=True)
     t0 = time.perf_counter()
@@ -214,16 +240,47 @@ def confirm_bench(se, ev, final_tick, batch, dev):
     audio = se.normalize_events(pos)
     t1 = time.perf_counter()
     wc = WhisperConfirm(device=dev)
-    wc.transcribe(audio[:2])                        # warm-up (kernels, allocator)
+    wc.transcribe(audio)                            # warm-up at the timed shape (kernels, allocator)
     torch.cuda.synchronize()
+    reps = 3
     t2 = time.perf_counter()
-    wc.transcribe(audio)
+    for _ in range(reps):
+        wc.transcribe(audio)
     torch.cuda.synchronize()
     t3 = time.perf_counter()
-    return {"segments": int(len(pos)), "normalize_ms": (t1 - t0) * 1e3, "whisper_batch_ms": (t3 - t2) * 1e3,
-            "segments_per_s": len(pos) / (t3 - t2 + t1 - t0), "max_new_tokens": wc.max_new_tokens,
+    whisper_s = (t3 - t2) / reps
+    return {"segments": int(len(pos)), "normalize_ms": (t1 - t0) * 1e3, "whisper_batch_ms": whisper_s * 1e3,
+            "segments_per_s": len(pos) / (whisper_s + t1 - t0), "max_new_tokens": wc.max_new_tokens,
             "model": "whisper-tiny dims (transformers WhisperConfig default), random init: no weights offline "
                      "(timing only, parity unpinned)"}
+
+
+def fixed_length_bench(torch, dev, ewa, eng, word, n_seg, seed, sh, fixed_len=16000, reps=5):
+    """Scorer kernel on n_seg segments of one fixed length (L = 16000, T = 101 frames each)."""
+    pcm, d_off, d_len, frames, _, _ = make_segments(torch, dev, n_seg, seed + 17, word, fixed_len=fixed_len)
+    mean = torch.empty((n_seg, 20), device=dev, dtype=torch.float32)
+    std = torch.empty((n_seg, 20), device=dev, dtype=torch.float32)
+    score = torch.empty(n_seg, device=dev, dtype=torch.float64)
+    match = torch.empty(n_seg, device=dev, dtype=torch.uint8)
+
+    def step():
+        eng.score_device(pcm.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n_seg, mean.data_ptr(),
+                         std.data_ptr(), score.data_ptr(), match.data_ptr(), sh)
+
+    step()
+    torch.cuda.synchronize()
+    eng.profile(True)
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize()
+    k_ms, k_n = eng.profile_read(0)
+    eng.profile(False)
+    ms = k_ms / max(1, k_n)
+    out = {"segment_samples": fixed_len, "segments": n_seg, "frames_per_launch": frames, "kernel_ms": ms,
+           "frames_per_s": frames / (ms / 1e3), "roofline_frac": frames * BYTES_PER_FRAME / (ms / 1e3) / (HBM_PEAK_GBS * 1e9),
+           "matches": int(match.sum().item())}
+    del pcm
+    return out
 
 
 def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1, first_stream=0, cdev=None,
@@ -239,14 +296,14 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
     rng = np.random.Generator(np.random.PCG64(seed + 11))
     sig = torch.from_numpy(rng.uniform(1e-4, 3e-3, n_streams).astype(np.float32)).to(dev)
     pcm = torch.randn((n_streams, P), generator=g, device=dev, dtype=torch.float32) * sig[:, None]
-    wv = torch.from_numpy(word).to(dev)
     wl = len(word)
-    # five events per 16 s loop per stream at jittered positions: words and distractors
+    table = torch.from_numpy(event_sources(word, rng)).to(dev)
+    # five events per 16 s loop per stream at jittered positions: half words, half distractors
     for e in range(5):
         pos = (e * P // 5 + rng.integers(0, 8000, n_streams)).astype(np.int64)
         gain = torch.from_numpy(rng.uniform(0.3, 2.0, n_streams).astype(np.float32)).to(dev)
-        rev = torch.from_numpy(rng.random(n_streams) < 0.3).to(dev)
-        src = torch.where(rev[:, None], wv.flip(0)[None, :], wv[None, :]) * gain[:, None]
+        kind = event_kind(rng, n_streams)
+        src = table[torch.from_numpy(kind).to(dev)] * gain[:, None]
         idx = torch.from_numpy(pos).to(dev)[:, None] + torch.arange(wl, device=dev)[None, :]
         pcm.scatter_add_(1, idx, src)
     torch.cuda.synchronize()
@@ -393,6 +450,8 @@ def main():
     n_match = int(match.sum().item())
     n_nan = int(torch.isnan(score).sum().item())
 
+    fixed = fixed_length_bench(torch, dev, ewa, eng, word, n_seg, args.seed + 1000 * rank, sh) \
+        if args.fixed_len > 0 and world == 1 else None
     kernel_s = (k_ms / max(1, k_n)) / 1e3
     achieved = frames * BYTES_PER_FRAME / kernel_s / 1e9
     traffic, traffic_src = None, None
@@ -443,6 +502,8 @@ def main():
         "matches_per_step": n_match,
         "nan_scores": n_nan,
     }
+    if fixed is not None:
+        out["fixed_length"] = fixed
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sample = min(n_seg, 16 * 400)
