@@ -950,6 +950,11 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
 #else
     uint64_t* tim = nullptr;
 #endif
+    // the template is loop-invariant: fetched once, off every segment's critical path.
+    // (Reserving the next work item ahead was tried: the tail imbalance costs more.)
+    const bool act = lane < NMFCC;
+    const float tmf = (a.has_template && act) ? a.tmpl[lane] : 0.0f;
+    const float tsf = (a.has_template && act) ? a.tmpl[NMFCC + lane] : 0.0f;
     for (;;) {
         EWK_TS(ta);
         int idx = 0;
@@ -1001,9 +1006,7 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
         }
         if (a.has_template) {
             // wave-parallel dots (fixed butterfly order), lane 0 finishes the score
-            const bool act = lane < NMFCC;
             const float cmf = act ? misc[lane] : 0.0f, csf = act ? misc[20 + lane] : 0.0f;
-            const float tmf = act ? a.tmpl[lane] : 0.0f, tsf = act ? a.tmpl[NMFCC + lane] : 0.0f;
             double score;
             if (a.cand_f32) {   // float32 candidates: float products, float-rounded dots (sdot)
                 const float uv_m = (float)wave_sum_d((double)(tmf * cmf)), vv_m = (float)wave_sum_d((double)(cmf * cmf));
