@@ -53,6 +53,11 @@ struct Tables64 {
     double sn[NFFT];         // sin(2*pi*n/512)
     float melw_dense[NMEL * NBIN];  // librosa float32 mel basis [128][257]
     double dct[NMFCC * NMEL];
+    // the basis's band support, packed: band m = weights mel_w[mel_off[m] .. mel_off[m+1])
+    // on bins mel_lo[m], mel_lo[m] + 1, ... (every non-zero weight, in bin order)
+    int32_t mel_lo[NMEL];
+    int32_t mel_off[NMEL + 1];
+    float mel_w[2 * NBIN + 2 * NMEL];
 };
 
 void build_tables(Tables* t);

@@ -1084,10 +1084,10 @@ hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mo
 
 // ============================================================================
 // fp64 reference-precision path (re-scoring near the decision threshold).
-// One 256-thread workgroup per segment; direct 512-point DFT per frame in fp64
-// with the float32-rounded librosa mel basis, fp64 log10, top_db clamp,
-// fp64 DCT and two-pass mean/std -- the float64 candidate path of the
-// reference (wakeword.py:1105-1121 hands float64 ring slices to librosa).
+// One 256-thread workgroup per segment; fp64 FFT per frame with the float32-
+// rounded librosa mel basis, fp64 log10, top_db clamp, fp64 DCT and two-pass
+// mean/std -- the float64 candidate path of the reference (wakeword.py:1105-1121
+// hands float64 ring slices to librosa).
 // ============================================================================
 // numpy's float64 pairwise add.reduce over n strided values (n <= 8192: one ufunc buffer)
 struct SegView {
@@ -1132,19 +1132,65 @@ __device__ double np_sum(const double* a, int n, int stride) {
     return acc;
 }
 
+// Wave-level radix-2 FFT of 256 complex doubles held in LDS in bit-reversed order
+// (the 512-point real frame as z[n] = x[2n] + i x[2n+1]); tw[k] = W256^k, k < 128.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ void fft256_f64(double2* z, const double2* tw, int lane) {
+#pragma unroll 1
+    for (int s = 0; s < 8; ++s) {
+        const int half = 1 << s;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int b = lane + 64 * j;                  // butterfly 0..127
+            const int pos = b & (half - 1);
+            const int i0 = ((b >> s) << (s + 1)) + pos, i1 = i0 + half;
+            const double2 w = tw[pos << (7 - s)];
+            const double2 u = z[i0], v = z[i1];
+            const double tr = v.x * w.x - v.y * w.y, ti = v.x * w.y + v.y * w.x;
+            z[i0] = make_double2(u.x + tr, u.y + ti);
+            z[i1] = make_double2(u.x - tr, u.y - ti);
+        }
+        wave_sync();
+    }
+}
+
+// One 256-thread workgroup per segment; its four waves take the frames in turn (fp64
+// FFT, packed-support mel, log10), then the workgroup clamps at max - 80 dB, runs the
+// fp64 DCT and numpy's pairwise mean / population std.
 template <int RING>
 __global__ __launch_bounds__(256) void k_score_f64(const Tables64* __restrict__ tb, ScoreArgs a,
                                                    double* scratch, int64_t per_seg,
                                                    double* out_mean64, double* out_std64) {
-    __shared__ double s_x[NFFT];
-    __shared__ double s_p[NBIN];
-    __shared__ double s_red[256];
+    __shared__ double2 s_z[4][256];
+    __shared__ double s_p[4][NBIN + 3];
+    __shared__ double s_win[NFFT];
+    __shared__ double2 s_tw[128];          // W256^k
+    __shared__ double2 s_cs[NBIN];         // (cos, sin)(2 pi k / 512), k <= 256
+    __shared__ double s_dct[NMFCC * NMEL];
+    __shared__ float s_mw[2 * NBIN + 2 * NMEL];
+    __shared__ int s_mlo[NMEL], s_moff[NMEL + 1];
+    __shared__ double s_red[4];
     __shared__ double s_stat[2 * NMFCC];
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    for (int i = tid; i < NFFT; i += 256) s_win[i] = tb->win[i];
+    for (int i = tid; i < 128; i += 256) s_tw[i] = make_double2(tb->cs[2 * i], -tb->sn[2 * i]);   // W256^i = W512^2i
+    for (int i = tid; i < NBIN; i += 256) s_cs[i] = make_double2(tb->cs[i], tb->sn[i]);
+    for (int i = tid; i < NMFCC * NMEL; i += 256) s_dct[i] = tb->dct[i];
+    for (int i = tid; i < 2 * NBIN + 2 * NMEL; i += 256) s_mw[i] = tb->mel_w[i];
+    for (int i = tid; i < NMEL; i += 256) s_mlo[i] = tb->mel_lo[i];
+    for (int i = tid; i <= NMEL; i += 256) s_moff[i] = tb->mel_off[i];
+    __syncthreads();
     int count;
     if (a.rescore_list) count = min(*a.rescore_count, a.rescore_cap);
     else count = RING ? min(a.n_seg, *a.n_events) : a.n_seg;
     double* lm = scratch + (int64_t)blockIdx.x * per_seg;   // [T][128] log-mel, then [T][20] mfcc
+    double2* z = s_z[wave];
+    double* pw = s_p[wave];
     for (int w = blockIdx.x; w < count; w += gridDim.x) {
         const int seg = a.rescore_list ? a.rescore_list[w] : w;
         SegView v;
@@ -1163,47 +1209,53 @@ __global__ __launch_bounds__(256) void k_score_f64(const Tables64* __restrict__ 
         const int T = 1 + v.len / HOP;
         if ((int64_t)T * (NMEL + NMFCC) > per_seg) continue;   // host sizes scratch; never expected
         double lmax = -INFINITY;
-        for (int t = 0; t < T; ++t) {
-            for (int n = tid; n < NFFT; n += 256) s_x[n] = tb->win[n] * (double)seg_sample(v, t * HOP - NFFT / 2 + n);
-            __syncthreads();
-            {   // bins tid (0..255) and 256 (thread 0)
-                const int k = tid;
-                double re = 0.0, im = 0.0;
-                for (int n = 0; n < NFFT; ++n) {
-                    const int idx = (n * k) & (NFFT - 1);
-                    re = fma(s_x[n], tb->cs[idx], re);
-                    im = fma(-s_x[n], tb->sn[idx], im);
-                }
-                s_p[k] = re * re + im * im;
-                if (tid == 0) {
-                    double r = 0.0;
-                    for (int n = 0; n < NFFT; ++n) r += (n & 1) ? -s_x[n] : s_x[n];
-                    s_p[256] = r * r;
-                }
+        for (int t = wave; t < T; t += 4) {
+            // windowed z[n] = x[2n] + i x[2n+1], stored bit-reversed for the in-place FFT
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int n = lane + 64 * j;
+                const int q = t * HOP - NFFT / 2 + 2 * n;
+                z[__brev((unsigned)n) >> 24] = make_double2(s_win[2 * n] * (double)seg_sample(v, q),
+                                                            s_win[2 * n + 1] * (double)seg_sample(v, q + 1));
             }
-            __syncthreads();
-            if (tid < NMEL) {
-                const float* wrow = tb->melw_dense + tid * NBIN;
+            wave_sync();
+            fft256_f64(z, s_tw, lane);
+            // untangle: X[k] = E[k] + W512^k O[k], E = (Z[k] + conj Z[256-k]) / 2,
+            // O = (Z[k] - conj Z[256-k]) / 2i;  P[k] = |X[k]|^2, k = 0..256
+            for (int k = lane; k < NBIN; k += 64) {
+                const double2 zk = z[k & 255], zc = z[(256 - k) & 255];
+                const double er = 0.5 * (zk.x + zc.x), ei = 0.5 * (zk.y - zc.y);
+                const double orr = 0.5 * (zk.y + zc.y), oi = -0.5 * (zk.x - zc.x);
+                const double2 cs = s_cs[k];   // W512^k = cos - i sin
+                const double xr = er + (orr * cs.x + oi * cs.y);
+                const double xi = ei + (oi * cs.x - orr * cs.y);
+                pw[k] = xr * xr + xi * xi;
+            }
+            wave_sync();
+            // mel (every non-zero weight of the band, in bin order: the dense dot's value)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int m = lane + 64 * h;
+                const int lo = s_mlo[m], o0 = s_moff[m], o1 = s_moff[m + 1];
                 double acc = 0.0;
-                for (int k = 0; k < NBIN; ++k) acc = fma((double)wrow[k], s_p[k], acc);
+                for (int o = o0; o < o1; ++o) acc = fma((double)s_mw[o], pw[lo + o - o0], acc);
                 const double db = 10.0 * log10(fmax(1e-10, acc));
-                lm[(int64_t)t * NMEL + tid] = db;
-                s_red[tid] = db;
+                lm[(int64_t)t * NMEL + m] = db;
+                lmax = fmax(lmax, db);
             }
-            __syncthreads();
-            if (tid == 0) for (int m = 0; m < NMEL; ++m) lmax = fmax(lmax, s_red[m]);
-            __syncthreads();
+            wave_sync();
         }
-        if (tid == 0) s_red[0] = lmax;
+        for (int o = 32; o > 0; o >>= 1) lmax = fmax(lmax, __shfl_xor(lmax, o, 64));
+        if (lane == 0) s_red[wave] = lmax;
         __syncthreads();
-        const double theta = s_red[0] - 80.0;
-        __syncthreads();
+        const double theta = fmax(fmax(s_red[0], s_red[1]), fmax(s_red[2], s_red[3])) - 80.0;
         double* mf = lm + (int64_t)T * NMEL;
         for (int i = tid; i < T * NMFCC; i += 256) {
             const int t = i / NMFCC, k = i % NMFCC;
             const double* row = lm + (int64_t)t * NMEL;
+            const double* dk = s_dct + k * NMEL;
             double acc = 0.0;
-            for (int m = 0; m < NMEL; ++m) acc = fma(tb->dct[k * NMEL + m], fmax(row[m], theta), acc);
+            for (int m = 0; m < NMEL; ++m) acc = fma(dk[m], fmax(row[m], theta), acc);
             mf[i] = acc;
         }
         __syncthreads();

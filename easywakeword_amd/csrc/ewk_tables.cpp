@@ -132,6 +132,20 @@ void build_tables64(Tables64* t) {
     }
     mel_dense(t->melw_dense);
     dct_rows(t->dct);
+    int off = 0;
+    for (int m = 0; m < NMEL; ++m) {
+        int lo = -1, hi = -1;
+        for (int k = 0; k < NBIN; ++k)
+            if (t->melw_dense[m * NBIN + k] != 0.0f) {
+                if (lo < 0) lo = k;
+                hi = k;
+            }
+        if (lo < 0) { lo = 0; hi = -1; }
+        t->mel_lo[m] = lo;
+        t->mel_off[m] = off;
+        for (int k = lo; k <= hi && off < (int)(sizeof(t->mel_w) / sizeof(float)); ++k) t->mel_w[off++] = t->melw_dense[m * NBIN + k];
+    }
+    t->mel_off[NMEL] = off;
 }
 
 }  // namespace ewk
