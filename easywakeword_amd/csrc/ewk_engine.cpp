@@ -111,6 +111,17 @@ struct ewk_engine {
     bool bank_used[2] = {false, false};
     hipEvent_t bank_done[2] = {nullptr, nullptr};   // recorded after the last push into a bank
     hipStream_t cstream = nullptr;                  // D2H copies of drained banks
+    // Ring-mode scoring of tick t runs on sstream concurrently with the gate of tick t+1
+    // on `stream` (the gate only overwrites ring samples older than any scorable segment;
+    // see `overlap`).  At most one scoring pass is in flight beside a gate.
+    hipStream_t sstream = nullptr;
+    hipEvent_t gate_evt[2] = {nullptr, nullptr};
+    hipEvent_t score_evt[2] = {nullptr, nullptr};
+    bool score_live[2] = {false, false};
+    hipEvent_t score_tail = nullptr;                // the latest recorded score_evt
+    int64_t push_seq = 0;
+    bool overlap = false;
+    int32_t ticks_per_launch = 32;                  // gate launch length (segments must outlive it in the ring)
     ewk_event* ev_bank(int b) { return d_events + (size_t)b * ev_cap; }
     int32_t* evc_bank(int b) { return d_evc + 4 * b; }
     DevBuf<float> push_stage;
@@ -120,6 +131,7 @@ struct ewk_engine {
     hipEvent_t h_stage_free = nullptr;   // recorded after the last DMA out of h_stage
     int64_t tick = 0;
     int32_t gate_stage = 0;
+    int32_t gate_val_len = 0;       // per-wave LDS doubles of the gate (tree values, sort scratch)
 
     // measurement: (start, stop) event pairs per kernel family
     bool prof = false;
@@ -162,10 +174,19 @@ static void zero_event_state(ewk_engine* e) {
     e->bank_used[0] = e->bank_used[1] = false;
 }
 
+// Order stream s after every ring-mode scoring pass enqueued so far (they run on
+// sstream): needed before touching what those passes read or share -- the template,
+// the re-score list, the log-mel and fp64 scratch, the event banks.
+static hipError_t join_scoring(ewk_engine* e, hipStream_t s) {
+    if (!e->overlap || !e->score_tail) return hipSuccess;
+    return hipStreamWaitEvent(s, e->score_tail, 0);
+}
+
 // The re-score list holds at most one entry per segment of a launch.
 static hipError_t reserve_rescore(ewk_engine* e, int32_t n_seg) {
     if (n_seg <= e->rescore_cap) return hipSuccess;
     hipError_t err = hipStreamSynchronize(e->stream);
+    if (err == hipSuccess && e->sstream) err = hipStreamSynchronize(e->sstream);
     if (err != hipSuccess) return err;
     err = e->rescore_buf.reserve((size_t)n_seg + 1);
     if (err != hipSuccess) return err;
@@ -180,6 +201,7 @@ static hipError_t reserve_lm(ewk_engine* e, int32_t n_seg, int ring_mode) {
     const size_t need = waves * kLmTiles * 20 * 64;   // float2 units: 8 KB tile + 2 KB DCT columns
     if (need <= e->lm_scratch.cap) return hipSuccess;
     hipError_t err = hipStreamSynchronize(e->stream);
+    if (err == hipSuccess && e->sstream) err = hipStreamSynchronize(e->sstream);
     if (err != hipSuccess) return err;
     return e->lm_scratch.reserve(need);
 }
@@ -218,6 +240,7 @@ void ewk_destroy(ewk_engine* e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->sstream) (void)hipStreamSynchronize(e->sstream);
     (void)hipFree(e->d_tab);
     (void)hipFree(e->d_tab64);
     (void)hipFree(e->d_tmpl);
@@ -247,8 +270,12 @@ void ewk_destroy(ewk_engine* e) {
     if (e->h_stage_free) (void)hipEventDestroy(e->h_stage_free);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     if (e->cstream) (void)hipStreamDestroy(e->cstream);
-    for (int b = 0; b < 2; ++b)
+    if (e->sstream) (void)hipStreamDestroy(e->sstream);
+    for (int b = 0; b < 2; ++b) {
         if (e->bank_done[b]) (void)hipEventDestroy(e->bank_done[b]);
+        if (e->gate_evt[b]) (void)hipEventDestroy(e->gate_evt[b]);
+        if (e->score_evt[b]) (void)hipEventDestroy(e->score_evt[b]);
+    }
     delete e;
 }
 
@@ -291,6 +318,11 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
     hipError_t err;
     if ((err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking)) != hipSuccess) return bail(err, "stream");
     if ((err = hipStreamCreateWithFlags(&e->cstream, hipStreamNonBlocking)) != hipSuccess) return bail(err, "stream");
+    if ((err = hipStreamCreateWithFlags(&e->sstream, hipStreamNonBlocking)) != hipSuccess) return bail(err, "stream");
+    for (int b = 0; b < 2; ++b) {
+        if ((err = hipEventCreateWithFlags(&e->gate_evt[b], hipEventDisableTiming)) != hipSuccess) return bail(err, "event");
+        if ((err = hipEventCreateWithFlags(&e->score_evt[b], hipEventDisableTiming)) != hipSuccess) return bail(err, "event");
+    }
     for (int b = 0; b < 2; ++b)
         if ((err = hipEventCreateWithFlags(&e->bank_done[b], hipEventDisableTiming)) != hipSuccess)
             return bail(err, "event");
@@ -314,8 +346,9 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
     if ((err = hipMalloc(&e->d_tmpl, 2 * NMFCC * sizeof(float))) != hipSuccess) return bail(err, "template");
     if ((err = e->rescore_buf.reserve(1 + e->rescore_cap)) != hipSuccess) return bail(err, "rescore");
     e->d_rescore = e->rescore_buf.p;
-    if ((err = hipMalloc(&e->d_work, 4 * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
-    if ((err = hipMemset(e->d_work, 0, 4 * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
+    // [0] linear work counter, [1] ring work counter, [2] ring re-score count, [4..5] event-count snapshots
+    if ((err = hipMalloc(&e->d_work, 8 * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
+    if ((err = hipMemset(e->d_work, 0, 8 * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
     // fp64 scratch: log-mel + mfcc rows for the longest ring segment
     {
         const int64_t tmax = 1 + e->ring_len / HOP;
@@ -343,6 +376,7 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
             if ((err = hipMalloc(&e->d_trees, kNumTrees * sizeof(PwTree))) != hipSuccess) return bail(err, "trees");
             if ((err = hipMemcpy(e->d_trees, tr.data(), kNumTrees * sizeof(PwTree), hipMemcpyHostToDevice)) != hipSuccess)
                 return bail(err, "trees");
+            e->gate_val_len = gate_val_len(tr.data(), e->n_blocks);
         }
         e->ev_cap = std::max(4096, 4 * n_streams);
         if ((err = reserve_rescore(e, e->ev_cap)) != hipSuccess) return bail(err, "rescore list");
@@ -351,6 +385,17 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
             return bail(err, "events");
         if ((err = hipMalloc(&e->d_evc, 8 * sizeof(int32_t))) != hipSuccess) return bail(err, "event counters");
         e->gate_stage = gate_stage_len(c.block, e->n_last);
+        {   // overlap scoring with the next gate only if the next launch cannot reach a
+            // scorable segment: 2 launches of ticks + the longest segment and its trailing
+            // silence must fit in the ring
+            const double sr = (double)c.sample_rate;
+            const int64_t seg_max = (int64_t)(c.max_segment_seconds * sr) +
+                                    (int64_t)((c.post_speech_silence + c.padding + 2.0 * c.tick_seconds) * sr) + c.block;
+            const int64_t tpl = std::min<int64_t>(32, (e->ring_len - seg_max) / (2 * (int64_t)c.block));
+            const char* env = getenv("EWK_SCORE_OVERLAP");
+            e->overlap = tpl >= 1 && !(env && env[0] == '0');
+            e->ticks_per_launch = e->overlap ? (int32_t)tpl : 32;
+        }
         int rc = ewk_reset_streams(e);
         if (rc != EWK_OK) {
             std::string m = g_err;
@@ -366,6 +411,7 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
 int ewk_sync(ewk_engine* e) {
     if (!e) return fail(EWK_EINVAL, "engine is NULL");
     HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(hipStreamSynchronize(e->sstream));
     return EWK_OK;
 }
 
@@ -386,6 +432,7 @@ int ewk_set_template(ewk_engine* e, const float* mean20, const float* std20) {
         e->uu_s32 = (float)as;
     }
     HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(join_scoring(e, e->stream));
     HIP_TRY(hipMemcpyAsync(e->d_tmpl, e->h_tmpl, sizeof(e->h_tmpl), hipMemcpyHostToDevice, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
     e->has_tmpl = true;
@@ -467,6 +514,7 @@ int ewk_score_segments_device(ewk_engine* e, const float* d_pcm, const int64_t* 
     HIP_TRY(reserve_rescore(e, n_seg));
     HIP_TRY(reserve_lm(e, n_seg, 0));
     hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    HIP_TRY(join_scoring(e, s));
     return score_linear(e, d_pcm, d_offsets, d_lengths, n_seg, d_mean, d_std, d_score, d_match, flags, s);
 }
 
@@ -512,6 +560,7 @@ int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int
     HIP_TRY(e->score.reserve(n_seg));
     HIP_TRY(e->match.reserve(n_seg));
     hipStream_t s = e->stream;
+    HIP_TRY(join_scoring(e, s));
     if (n_pcm > 0) HIP_TRY(hipMemcpyAsync(e->pcm.p, pcm, n_pcm * sizeof(float), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(e->offsets.p, offsets, n_seg * sizeof(int64_t), hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(e->lengths.p, lengths, n_seg * sizeof(int32_t), hipMemcpyHostToDevice, s));
@@ -557,6 +606,7 @@ int ewk_score_segments_f64(ewk_engine* e, const float* pcm, int64_t n_pcm, const
     if (rc) return rc;
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = e->stream;
+    HIP_TRY(join_scoring(e, s));
     const int64_t tmax = std::max<int64_t>(1 + e->ring_len / HOP, 1 + max_len / HOP);
     const int64_t per = tmax * (NMEL + NMFCC);
     HIP_TRY(hipStreamSynchronize(s));
@@ -608,6 +658,7 @@ int ewk_reset_streams(ewk_engine* e) {
     if (e->n_streams <= 0) return EWK_OK;
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = e->stream;
+    HIP_TRY(join_scoring(e, s));
     HIP_TRY(hipMemsetAsync(e->d_ring, 0, (size_t)e->n_streams * e->ring_len * sizeof(float), s));
     HIP_TRY(hipMemsetAsync(e->d_brms, 0, (size_t)e->n_streams * std::max(1, e->n_blocks) * sizeof(double), s));
     std::vector<GateStream> st(e->n_streams);
@@ -625,28 +676,29 @@ int ewk_reset_streams(ewk_engine* e) {
 }
 
 // Score the events queued since the last scoring pass (ring mode), then advance the watermark.
-static int score_pending(ewk_engine* e) {
+// Score the current bank's events [ev_base, *n_events) on stream ss; n_events is the
+// live counter (same stream as the gate) or a snapshot of it taken after the gate.
+static int score_pending(ewk_engine* e, hipStream_t ss, const int32_t* n_events) {
     if (!e->has_tmpl) return EWK_OK;   // events keep NaN scores until a template exists
     ScoreArgs a = base_args(e);
     a.pcm = e->d_ring;
     a.ring_len = e->ring_len;
     a.events = e->ev_bank(e->bank);
-    a.n_events = e->evc_bank(e->bank);
+    a.n_events = n_events;
     a.ev_base = e->evc_bank(e->bank) + 2;
     a.n_seg = e->ev_cap;
     a.work = e->d_work + 1;            // ring-mode counters (zeroed at create, re-armed by k_advance)
     a.rescore_count = e->d_work + 2;
     {
-        ProfScope ps(e, 0, e->stream);
-        HIP_TRY(launch_score_f32(e->d_tab, a, 1, e->stream));
+        ProfScope ps(e, 0, ss);
+        HIP_TRY(launch_score_f32(e->d_tab, a, 1, ss));
     }
     const int64_t per = (1 + e->ring_len / HOP) * (NMEL + NMFCC);
     {
-        ProfScope ps(e, 1, e->stream);
-        HIP_TRY(launch_score_f64(e->d_tab64, a, 1, e->f64_scratch.p, per, e->f64_grid, nullptr, nullptr, e->stream));
+        ProfScope ps(e, 1, ss);
+        HIP_TRY(launch_score_f64(e->d_tab64, a, 1, e->f64_scratch.p, per, e->f64_grid, nullptr, nullptr, ss));
     }
-    HIP_TRY(launch_advance_watermark(e->evc_bank(e->bank) + 2, e->evc_bank(e->bank), e->d_work + 1, e->d_work + 2,
-                                     e->stream));
+    HIP_TRY(launch_advance_watermark(e->evc_bank(e->bank) + 2, n_events, e->d_work + 1, e->d_work + 2, ss));
     return EWK_OK;
 }
 
@@ -688,9 +740,9 @@ static int push_impl(ewk_engine* e, const void* pcm_any, int64_t stride, int64_t
         st_stride = (int64_t)per_stream;
         tk_stride = e->cfg.block;
     }
-    // Segments must be scored before the ring overwrites them: <= 32 ticks per gate launch.
-    for (int32_t t0 = 0; t0 < n_ticks; t0 += 32) {
-        const int32_t nt = std::min<int32_t>(32, n_ticks - t0);
+    // Segments must be scored before the ring overwrites them: <= ticks_per_launch ticks per gate launch.
+    for (int32_t t0 = 0; t0 < n_ticks; t0 += e->ticks_per_launch) {
+        const int32_t nt = std::min<int32_t>(e->ticks_per_launch, n_ticks - t0);
         GateArgs g;
         memset(&g, 0, sizeof(g));
         if (pcm16) g.pcm16 = static_cast<const int16_t*>(src) + (int64_t)t0 * tk_stride;
@@ -711,6 +763,7 @@ static int push_impl(ewk_engine* e, const void* pcm_any, int64_t stride, int64_t
         g.n_last = e->n_last;
         g.sample_rate = e->cfg.sample_rate;
         g.stage = e->gate_stage;
+        g.val_len = e->gate_val_len;
         g.tick_seconds = e->cfg.tick_seconds;
         g.pre_speech_silence = e->cfg.pre_speech_silence;
         g.speech_duration_min = e->cfg.speech_duration_min;
@@ -724,15 +777,32 @@ static int push_impl(ewk_engine* e, const void* pcm_any, int64_t stride, int64_t
         g.ev_count = e->evc_bank(e->bank);
         g.ev_dropped = e->evc_bank(e->bank) + 1;
         g.ev_cap = e->ev_cap;
+        const int k = (int)(e->push_seq & 1);
+        // the scoring pass two launches back must be done: it read snapshot slot k, and
+        // at most one pass runs beside a gate
+        if (e->overlap && e->score_live[k]) HIP_TRY(hipStreamWaitEvent(s, e->score_evt[k], 0));
         {
             ProfScope ps(e, 2, s);
             HIP_TRY(launch_gate(g, s));
         }
         e->tick += nt;
-        int rc = score_pending(e);
-        if (rc) return rc;
+        if (e->overlap) {
+            int32_t* snap = e->d_work + 4 + k;
+            HIP_TRY(launch_snapshot(e->evc_bank(e->bank), snap, s));
+            HIP_TRY(hipEventRecord(e->gate_evt[k], s));
+            HIP_TRY(hipStreamWaitEvent(e->sstream, e->gate_evt[k], 0));
+            int rc = score_pending(e, e->sstream, snap);
+            if (rc) return rc;
+            HIP_TRY(hipEventRecord(e->score_evt[k], e->sstream));
+            e->score_live[k] = true;
+            e->score_tail = e->score_evt[k];
+        } else {
+            int rc = score_pending(e, s, e->evc_bank(e->bank));
+            if (rc) return rc;
+        }
+        e->push_seq += 1;
     }
-    HIP_TRY(hipEventRecord(e->bank_done[e->bank], s));
+    HIP_TRY(hipEventRecord(e->bank_done[e->bank], e->overlap ? e->sstream : s));
     e->bank_used[e->bank] = true;
     return EWK_OK;
 }
@@ -759,6 +829,7 @@ int ewk_push_many_pcm16(ewk_engine* e, const int16_t* pcm, int64_t stride, int64
 static int normalize_impl(ewk_engine* e, const float* d_pcm, const int64_t* offsets, const int32_t* lengths,
                           const ewk_event* events, int32_t n, double* out, int32_t flags) {
     hipStream_t s = e->stream;
+    HIP_TRY(join_scoring(e, s));
     std::vector<int64_t> oo(n);
     int64_t total = 0;
     for (int32_t i = 0; i < n; ++i) {

@@ -75,6 +75,7 @@ struct GateArgs {
     int64_t n_last;          // int(0.1 * sample_rate)
     int32_t sample_rate;
     int32_t stage;           // per-wave LDS sample staging (floats); 0 = read the ring directly
+    int32_t val_len;         // per-wave LDS doubles: tree node values (and the register path's sort scratch)
     double tick_seconds;
     double pre_speech_silence, speech_duration_min, speech_duration_max, post_speech_silence;
     double padding, max_segment_seconds, reentry_timeout, min_threshold;
@@ -85,6 +86,9 @@ struct GateArgs {
 };
 
 hipError_t launch_gate(const GateArgs& g, hipStream_t s);
+// register-resident block RMS arrays up to 64 * kGateRegMax blocks (10 s ring: block >= 313 samples)
+constexpr int kGateRegMax = 8;
+int gate_val_len(const PwTree* trees_host, int n_blocks);
 // per-wave sample staging length for a config (0 when the lengths exceed the LDS budget)
 int gate_stage_len(int block, int64_t n_last);
 

@@ -36,7 +36,20 @@
 // float64 parity with numpy requires un-fused multiply/add (e.g. the percentile lerp)
 #pragma clang fp contract(off)
 
+#ifndef EWK_GATE_TIMING
+#define EWK_GATE_TIMING 0   // per-phase s_memtime accounting (scripts/mb_gate.py variants only)
+#endif
+
 namespace ewk {
+
+#if EWK_GATE_TIMING
+__device__ unsigned long long g_gtim[16];
+#define GT_TS(x) const uint64_t x = __builtin_amdgcn_s_memtime()
+#define GT_ACC(i, a, b) (gt[i] += (b) - (a))
+#else
+#define GT_TS(x)
+#define GT_ACC(i, a, b)
+#endif
 
 // ---- host: flatten numpy's pairwise recursion for one chunk --------------------
 static int split_point(int n) {
@@ -138,11 +151,40 @@ __device__ __forceinline__ double leaf_sumsq(const Src& src, int s, int n) {
 }
 
 // One chunk (n = t->n elements of src) in numpy's pairwise order, wave-parallel.
-// val: per-wave LDS scratch of 2 * kPwMaxLeaves doubles.  Uniform result.
+// val: per-wave LDS scratch of 10 * n_leaves doubles (node values, then the leaves'
+// 8 accumulators).  Each accumulator chain of a leaf runs on its own lane (numpy's
+// r[j] += x[i + j]^2, i = 8, 16, ...), a second step combines the eight in numpy's
+// order and adds the < 8 tail elements -- the same additions as leaf_sumsq.
+// Uniform result.
 template <typename Src>
 __device__ double tree_sumsq(const Src& src, const PwTree* t, int lane, double* val) {
     const int L = t->n_leaves;
-    for (int l = lane; l < L; l += 64) val[l] = leaf_sumsq(src, t->leaf_start[l], t->leaf_len[l]);
+    double* acc8 = val + 2 * L;
+    for (int q = lane; q < 8 * L; q += 64) {
+        const int l = q >> 3, j = q & 7;
+        const int s0 = t->leaf_start[l], n = t->leaf_len[l];
+        if (n >= 8) {
+            double r;
+            { const double x = src(s0 + j); r = x * x; }
+            const int lim = n - (n % 8);
+            for (int i = 8; i < lim; i += 8) { const double x = src(s0 + i + j); r += x * x; }
+            acc8[q] = r;
+        }
+    }
+    wave_sync();
+    for (int l = lane; l < L; l += 64) {
+        const int s0 = t->leaf_start[l], n = t->leaf_len[l];
+        double res;
+        if (n < 8) {
+            res = 0.0;
+            for (int i = 0; i < n; ++i) { const double x = src(s0 + i); res += x * x; }
+        } else {
+            const double* r = acc8 + 8 * l;
+            res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+            for (int i = n - (n % 8); i < n; ++i) { const double x = src(s0 + i); res += x * x; }
+        }
+        val[l] = res;
+    }
     wave_sync();
     int b = 0;
     for (int h = 0; h < t->n_levels; ++h) {
@@ -219,30 +261,149 @@ __device__ __forceinline__ double percentile25_sorted(const double* sorted, int 
     return r;
 }
 
-__global__ __launch_bounds__(256) void k_gate_ticks(GateArgs g) {
+#ifndef EWK_GATE_WPE
+#define EWK_GATE_WPE 4
+#endif
+constexpr int kIngestLoads = 16;   // tick samples per lane loaded before the ring stores
+
+// ---- register-resident block RMS multiset (n_blocks <= 64 * RB) ------------------
+// Element i of a per-stream array lives in lane i % 64, slot i / 64.
+template <int RB>
+__device__ __forceinline__ double reg_get(const double (&v)[RB], int i) {
+    double r = 0.0;
+#pragma unroll
+    for (int j = 0; j < RB; ++j)
+        if ((i >> 6) == j) r = __shfl(v[j], i & 63, 64);
+    return r;
+}
+
+template <int RB>
+__device__ __forceinline__ void reg_set(double (&v)[RB], int i, double x, int lane) {
+#pragma unroll
+    for (int j = 0; j < RB; ++j)
+        if ((i >> 6) == j && lane == (i & 63)) v[j] = x;
+}
+
+// so (sorted, nb values) with one occurrence of vo replaced by vn, kept sorted: the
+// new element d comes from old element d - 1, d or d + 1 (or is vn), so the update is
+// two neighbour shuffles.  Returns false when vo is absent (caller re-sorts).
+template <int RB>
+__device__ bool reg_replace(double (&so)[RB], int nb, double vo, double vn, int lane) {
+    int pos = nb;
+#pragma unroll
+    for (int j = RB - 1; j >= 0; --j) {
+        const unsigned long long m = __ballot(lane + 64 * j < nb && so[j] == vo);
+        if (m) pos = 64 * j + __ffsll((long long)m) - 1;
+    }
+    if (pos >= nb) return false;
+    int cnt = 0;
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+        const int i = lane + 64 * j;
+        cnt += __popcll(__ballot(i < nb && i != pos && so[j] < vn));
+    }
+    double prev[RB], next[RB];
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+        const double up = __shfl(so[j], (lane + 63) & 63, 64);    // element d - 1 (lane 0: slot j-1's lane 63)
+        const double dn = __shfl(so[j], (lane + 1) & 63, 64);     // element d + 1 (lane 63: slot j+1's lane 0)
+        prev[j] = up;
+        next[j] = dn;
+    }
+    // the cross-slot neighbours for lane 0 / lane 63 (wave-uniform shuffles)
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+        const double tail = j > 0 ? __shfl(so[j - 1], 63, 64) : 0.0;
+        const double head = j + 1 < RB ? __shfl(so[j + 1], 0, 64) : 0.0;
+        if (lane == 0) prev[j] = tail;
+        if (lane == 63) next[j] = head;
+    }
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+        const int d = lane + 64 * j;
+        const int i1 = d < cnt ? d : d - 1;
+        const int i = i1 < pos ? i1 : i1 + 1;
+        const double x = i == d ? so[j] : (i < d ? prev[j] : next[j]);
+        so[j] = d == cnt ? vn : x;
+    }
+    return true;
+}
+
+// First fill / repair: so = sorted copy of gr (stable rank sort through LDS scratch tmp[nb]).
+template <int RB>
+__device__ void reg_rank_sort(const double (&gr)[RB], double (&so)[RB], int nb, double* tmp, int lane) {
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+        const int i = lane + 64 * j;
+        const double x = gr[j];
+        int r = 0;
+#pragma unroll
+        for (int jj = 0; jj < RB; ++jj)
+            for (int kk = 0; kk < 64; ++kk) {
+                const int k = 64 * jj + kk;
+                const double y = __shfl(gr[jj], kk, 64);
+                r += k < nb && ((y < x) || (y == x && k < i));
+            }
+        if (i < nb) tmp[r] = x;
+    }
+    wave_sync();
+#pragma unroll
+    for (int j = 0; j < RB; ++j) {
+        const int i = lane + 64 * j;
+        so[j] = i < nb ? tmp[i] : 0.0;
+    }
+    wave_sync();
+}
+
+// numpy.percentile(v, 25) ("linear") from the register-resident sorted copy.
+template <int RB>
+__device__ __forceinline__ double reg_percentile25(const double (&so)[RB], int nb) {
+    const double q = 0.25;
+    const double vi = (double)nb * q + (1.0 + q * (1.0 - 1.0 - 1.0)) - 1.0;
+    const double prevd = floor(vi);
+    int prev = (int)prevd, next = prev + 1;
+    if (vi >= (double)(nb - 1)) { prev = nb - 1; next = nb - 1; }
+    if (vi < 0.0) { prev = 0; next = 0; }
+    const double gamma = vi - prevd;
+    const double a = reg_get(so, prev), b = reg_get(so, next);
+    const double d = b - a;
+    double r = a + d * gamma;
+    if (gamma >= 0.5) r = b - d * (1.0 - gamma);
+    return r;
+}
+
+// RB > 0: the stream's block RMS array and its sorted copy live in registers for the
+// whole launch (RB slots per lane, n_blocks <= 64 * RB): loaded once, updated with
+// wave shuffles, stored once -- no dependent global round trips per tick.  RB = 0:
+// both stay in global memory (any n_blocks).
+template <int RB>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WPE, 8))) void k_gate_ticks(GateArgs g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    // pairwise trees (shared by the workgroup)
-    PwTree* trees = reinterpret_cast<PwTree*>(smem);
-    {
-        const int4* src = reinterpret_cast<const int4*>(g.trees);
-        int4* dst = reinterpret_cast<int4*>(smem);
-        for (int i = threadIdx.x; i < (int)(kNumTrees * sizeof(PwTree) / 16); i += blockDim.x) dst[i] = src[i];
-    }
-    __syncthreads();
+    const PwTree* __restrict__ trees = g.trees;   // read-only, cache-resident
     const int s = blockIdx.x * 4 + wave;
     if (s >= g.n_streams) return;
-    const size_t tree_bytes = (kNumTrees * sizeof(PwTree) + 15) & ~(size_t)15;
-    const size_t per_wave = (size_t)2 * kPwMaxLeaves * 8 + (size_t)g.stage * 4;
-    unsigned char* w = smem + tree_bytes + wave * per_wave;
+    const size_t per_wave = (size_t)g.val_len * 8 + (size_t)g.stage * 4;
+    unsigned char* w = smem + wave * per_wave;
     double* val = reinterpret_cast<double*>(w);
-    float* stage = reinterpret_cast<float*>(w + 2 * kPwMaxLeaves * 8);
+    float* stage = reinterpret_cast<float*>(w + (size_t)g.val_len * 8);
 
     const int R = (int)g.ring_len;
     const int fs = g.block;
     const int nb = g.n_blocks;
     const int nl = (int)min<int64_t>(g.n_last, g.ring_len);
     float* ring = g.ring + (int64_t)s * R;
+    // the first tick's samples are requested before the state: no load waits on another
+    float xin[kIngestLoads];
+    auto load_chunk = [&](int t, int c0) {
+        const int64_t so = (int64_t)s * g.stride + (int64_t)t * g.tick_stride;
+#pragma unroll
+        for (int m = 0; m < kIngestLoads; ++m) {
+            const int i = c0 + lane + 64 * m;
+            xin[m] = i < fs ? (g.pcm16 ? (float)g.pcm16[so + i] * (1.0f / 32768.0f) : g.pcm[so + i]) : 0.0f;
+        }
+    };
+    load_chunk(0, 0);
     GateStream st = g.st[s];
     double* grms = g.block_rms + (int64_t)s * nb;
     double* sorted2 = g.sorted_rms + (int64_t)s * 2 * nb;
@@ -251,8 +412,25 @@ __global__ __launch_bounds__(256) void k_gate_ticks(GateArgs g) {
     const PwTree* tlf = trees + kTreeLastFull;
     const PwTree* tlr = trees + kTreeLastRem;
     const bool staged = g.stage >= fs && g.stage >= nl;
+#if EWK_GATE_TIMING
+    uint64_t gt[8] = {};
+#endif
+    GT_TS(q_begin);
+    constexpr int RBn = RB > 0 ? RB : 1;
+    double gr[RBn], srt[RBn];
+    if (RB > 0) {   // (this path never double-buffers: sorted_sel stays 0)
+#pragma unroll
+        for (int j = 0; j < RBn; ++j) {
+            const int i = lane + 64 * j;
+            gr[j] = i < nb ? grms[i] : 0.0;
+            srt[j] = i < nb ? sorted2[i] : 0.0;
+        }
+    }
 
+    GT_TS(q_loaded);
+    GT_ACC(0, q_begin, q_loaded);
     for (int t = 0; t < g.n_ticks; ++t) {
+        GT_TS(q0);
         const int64_t tick = g.tick0 + t + 1;                    // tick being delivered
         const double t_prev = (double)(tick - 1) * g.tick_seconds;
         // start()-mode re-entry (TimeoutError -> _detect_word again), before the sleep
@@ -263,23 +441,32 @@ __global__ __launch_bounds__(256) void k_gate_ticks(GateArgs g) {
             st.reentries += 1;
         }
         // ---- a1: ingest `fs` samples at the write pointer (and stage them in LDS)
-        const int64_t so = (int64_t)s * g.stride + (int64_t)t * g.tick_stride;
-        const float* src = g.pcm + so;
-        const int16_t* src16 = g.pcm16 + so;
         const int p0 = st.pointer;
-        for (int i = lane; i < fs; i += 64) {
-            const float x = g.pcm16 ? (float)src16[i] * (1.0f / 32768.0f) : src[i];
-            int k = p0 + i;
-            if (k >= R) k -= R;
-            ring[k] = x;
-            if (staged) stage[i] = x;
+        // chunks of kIngestLoads loads per lane in flight before any store (the ring may
+        // alias the input as far as the compiler knows: a load-store loop serialises them);
+        // chunk 0 of this tick was requested before the previous tick's compute
+        for (int c0 = 0; c0 < fs; c0 += 64 * kIngestLoads) {
+            if (c0 > 0) load_chunk(t, c0);
+#pragma unroll
+            for (int m = 0; m < kIngestLoads; ++m) {
+                const int i = c0 + lane + 64 * m;
+                if (i < fs) {
+                    int k = p0 + i;
+                    if (k >= R) k -= R;
+                    ring[k] = xin[m];
+                    if (staged) stage[i] = xin[m];
+                }
+            }
         }
+        if (t + 1 < g.n_ticks) load_chunk(t + 1, 0);   // next tick's samples, in flight during this tick
         __threadfence_block();
         wave_sync();
         const bool wrapped = p0 + fs > R;
         st.pointer = (int32_t)((p0 + fs) % R);
         st.collected = min(st.collected + (int64_t)fs, (int64_t)R);
         const bool full = st.collected >= R;
+        GT_TS(q1);
+        GT_ACC(1, q0, q1);
         // block sum of the window when it coincides with a refreshed block
         double reuse_sum = 0.0;
         bool have_reuse = false;
@@ -294,11 +481,13 @@ __global__ __launch_bounds__(256) void k_gate_ticks(GateArgs g) {
             if (!st.filled) {
                 for (int b = 0; b < nb; ++b) {
                     const double sum = block_sum(b);
-                    if (lane == 0) grms[b] = sqrt(sum / (double)fs);
+                    if (RB > 0) reg_set(gr, b, sqrt(sum / (double)fs), lane);
+                    else if (lane == 0) grms[b] = sqrt(sum / (double)fs);
                 }
                 __threadfence_block();
                 wave_sync();
-                rank_sort(grms, sorted2, nb, lane);
+                if (RB > 0) reg_rank_sort(gr, srt, nb, val, lane);
+                else rank_sort(grms, sorted2, nb, lane);
                 st.sorted_sel = 0;
                 st.filled = 1;
             } else {
@@ -312,6 +501,12 @@ __global__ __launch_bounds__(256) void k_gate_ticks(GateArgs g) {
                         if (nl == fs && b * fs + fs == (int)st.pointer + (st.pointer == 0 ? R : 0)) {
                             reuse_sum = sum;
                             have_reuse = true;
+                        }
+                        if (RB > 0) {
+                            const double vo = reg_get(gr, b);
+                            reg_set(gr, b, v, lane);
+                            if (!reg_replace(srt, nb, vo, v, lane)) reg_rank_sort(gr, srt, nb, val, lane);
+                            continue;
                         }
                         const double vo = grms[b];
                         if (lane == 0) grms[b] = v;
@@ -332,13 +527,20 @@ __global__ __launch_bounds__(256) void k_gate_ticks(GateArgs g) {
                 if (!wrapped) refresh(p0, p0 + fs);
                 else { refresh(p0, R); refresh(0, p0 + fs - R); }
             }
-            __threadfence_block();
-            wave_sync();
-            const double p25 = percentile25_sorted(sorted2 + (int64_t)st.sorted_sel * nb, nb);
+            double p25;
+            if (RB > 0) {
+                p25 = reg_percentile25(srt, nb);
+            } else {
+                __threadfence_block();
+                wave_sync();
+                p25 = percentile25_sorted(sorted2 + (int64_t)st.sorted_sel * nb, nb);
+            }
             const double thr = p25 * 1.5;
             // Python max(new, MIN): MIN only if MIN > new
             st.threshold = (g.min_threshold > thr) ? g.min_threshold : thr;
         }
+        GT_TS(q2);
+        GT_ACC(2, q1, q2);
         // ---- a3: is_silent(): RMS of the last n_last samples < threshold
         bool silent = true;
         if (nl > 0) {
@@ -361,6 +563,8 @@ __global__ __launch_bounds__(256) void k_gate_ticks(GateArgs g) {
             st.last_rms = rms;
             silent = rms < st.threshold;
         }
+        GT_TS(q3);
+        GT_ACC(3, q2, q3);
         st.last_silent = silent;
         st.tick = tick;
         const double now = (double)tick * g.tick_seconds;
@@ -434,16 +638,54 @@ __global__ __launch_bounds__(256) void k_gate_ticks(GateArgs g) {
         st.sound_start = __shfl(st.sound_start, 0, 64);
         st.sound_end = __shfl(st.sound_end, 0, 64);
     }
+    GT_TS(q_loop);
+    GT_ACC(4, q_loaded, q_loop);
+    if (RB > 0 && st.filled) {
+#pragma unroll
+        for (int j = 0; j < RBn; ++j) {
+            const int i = lane + 64 * j;
+            if (i < nb) { grms[i] = gr[j]; sorted2[i] = srt[j]; }
+        }
+    }
     if (lane == 0) g.st[s] = st;
+#if EWK_GATE_TIMING
+    GT_TS(q_end);
+    GT_ACC(5, q_loop, q_end);
+    GT_ACC(6, q_begin, q_end);
+    if (lane == 0) {
+        for (int i = 0; i < 7; ++i) atomicAdd(&g_gtim[i], (unsigned long long)gt[i]);
+        atomicAdd(&g_gtim[7], 1ull);
+    }
+#endif
+}
+
+int gate_val_len(const PwTree* trees_host, int n_blocks) {
+    int m = 0;
+    for (int k = 0; k < kNumTrees; ++k) m = std::max(m, 10 * trees_host[k].n_leaves);
+    if (n_blocks <= 64 * kGateRegMax) m = std::max(m, n_blocks);   // register path's rank-sort scratch
+    return std::max(2, (m + 1) & ~1);
 }
 
 hipError_t launch_gate(const GateArgs& g, hipStream_t s) {
     if (g.n_streams <= 0 || g.n_ticks <= 0) return hipSuccess;
     const int grid = (g.n_streams + 3) / 4;
-    const size_t tree_bytes = (kNumTrees * sizeof(PwTree) + 15) & ~(size_t)15;
-    const size_t per_wave = (size_t)2 * kPwMaxLeaves * 8 + (size_t)g.stage * 4;
-    hipLaunchKernelGGL(k_gate_ticks, dim3(grid), dim3(256), tree_bytes + 4 * per_wave, s, g);
+    const size_t per_wave = (size_t)g.val_len * 8 + (size_t)g.stage * 4;
+    const size_t lds = 4 * per_wave;
+    if (g.n_blocks <= 128)
+        hipLaunchKernelGGL(k_gate_ticks<2>, dim3(grid), dim3(256), lds, s, g);
+    else if (g.n_blocks <= 64 * kGateRegMax)
+        hipLaunchKernelGGL(k_gate_ticks<kGateRegMax>, dim3(grid), dim3(256), lds, s, g);
+    else
+        hipLaunchKernelGGL(k_gate_ticks<0>, dim3(grid), dim3(256), lds, s, g);
     return hipGetLastError();
 }
 
 }  // namespace ewk
+
+#if EWK_GATE_TIMING
+extern "C" int ewk_debug_gate_timing(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ewk::g_gtim), 16 * sizeof(unsigned long long)) != hipSuccess) return -3;
+    unsigned long long z[16] = {};
+    return hipMemcpyToSymbol(HIP_SYMBOL(ewk::g_gtim), z, sizeof(z)) == hipSuccess ? 0 : -3;
+}
+#endif

@@ -1064,6 +1064,15 @@ hipError_t launch_advance_watermark(int32_t* ev_base, const int32_t* n_events, i
     return hipGetLastError();
 }
 
+// Event-count snapshot taken on the gate's stream right after a gate launch: the
+// scoring pass that overlaps the next gate scores exactly the events of its own tick.
+__global__ void k_snapshot(const int32_t* src, int32_t* dst) { *dst = *src; }
+
+hipError_t launch_snapshot(const int32_t* src, int32_t* dst, hipStream_t s) {
+    hipLaunchKernelGGL(k_snapshot, dim3(1), dim3(1), 0, s, src, dst);
+    return hipGetLastError();
+}
+
 int score_grid(int n_seg, int ring_mode) {
     return ring_mode ? kScoreGridRing : max(1, min((n_seg + WAVES - 1) / WAVES, kScoreGridMax));
 }
