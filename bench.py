@@ -340,17 +340,25 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
     t = run(0, 100, 32)                      # prefill (ring fill + detection start)
     se.sync()
     events.clear()
-    se.profile(True)
     torch.cuda.synchronize()
     w0 = time.perf_counter()
     t = run(t, n_ticks, 1, lagged=True)      # one tick per call: the real-time cadence, pipelined
     events.append(se.poll())                 # the last tick's events
     se.sync()
     wall = time.perf_counter() - w0
+    ev = np.concatenate(events) if events else np.zeros(0, dtype=se.poll().dtype)
+    # per-kernel times from a separate instrumented pass (event records stay out of the timed wall)
+    events.clear()
+    prof_ticks = min(200, n_ticks)
+    se.profile(True)
+    t = run(t, prof_ticks, 1, lagged=True)
+    events.append(se.poll())
+    se.sync()
     gate_ms, gate_n = se.profile_read(2)
     sc_ms, sc_n = se.profile_read(0)
     r_ms, r_n = se.profile_read(1)
-    ev = np.concatenate(events) if events else np.zeros(0, dtype=se.poll().dtype)
+    se.profile(False)
+    ev_latest = np.concatenate(events) if events else ev
     per_tick = wall / n_ticks
     real = ev[(ev["flags"] & 1) == 0]
     out = {"streams": n_streams, "ticks": n_ticks, "audio_seconds_per_stream": n_ticks * 0.1,
@@ -358,13 +366,15 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
            "realtime_factor": 0.1 / per_tick,
            "streams_realtime": n_streams * 0.1 / per_tick,
            "gate_kernel_ms_per_tick": gate_ms / max(1, gate_n),
-           "scorer_kernel_ms_per_tick": (sc_ms + r_ms) / max(1, sc_n),
+           "scorer_kernel_ms_per_tick": sc_ms / max(1, sc_n),
+           "rescore_kernel_ms_per_tick": r_ms / max(1, r_n),
+           "kernel_times": f"separate instrumented pass of {prof_ticks} ticks",
            "events": int(len(real)), "matches": int(real["match"].sum()) if len(real) else 0,
            "mfcc_frames": int((1 + real["length"].astype(np.int64) // HOP).sum()) if len(real) else 0}
     if world > 1:
         out["positives_gathered_to_rank0"] = gathered[0]
     if confirm_batch > 0:   # config 5: level 3 on the latest positives still in the rings
-        out["confirm"] = confirm_bench(se, ev, t, confirm_batch, dev)
+        out["confirm"] = confirm_bench(se, ev_latest, t, confirm_batch, dev)
     se.close()
     del pcm
     return out

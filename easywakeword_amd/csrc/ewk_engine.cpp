@@ -392,8 +392,10 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
             const int64_t seg_max = (int64_t)(c.max_segment_seconds * sr) +
                                     (int64_t)((c.post_speech_silence + c.padding + 2.0 * c.tick_seconds) * sr) + c.block;
             const int64_t tpl = std::min<int64_t>(32, (e->ring_len - seg_max) / (2 * (int64_t)c.block));
+            // opt-in (EWK_SCORE_OVERLAP=1): measured on MI355X the extra stream/event calls
+            // per tick cost more host time than the concurrency saves (scripts/mb_stream.py)
             const char* env = getenv("EWK_SCORE_OVERLAP");
-            e->overlap = tpl >= 1 && !(env && env[0] == '0');
+            e->overlap = tpl >= 1 && env && env[0] == '1';
             e->ticks_per_launch = e->overlap ? (int32_t)tpl : 32;
         }
         int rc = ewk_reset_streams(e);

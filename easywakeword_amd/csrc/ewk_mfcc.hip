@@ -84,7 +84,8 @@ constexpr int W_TILE = W_SCR + kScrFloats * 4;            // 16 x 128 floats, XO
 constexpr int W_MISC = W_SCR;                             // 64 floats, aliases the FFT scratch (epilogue only)
 constexpr int W_TMIN = W_TILE + 16 * NMEL * 4;            // per-tile log-mel minima (kLmTiles floats)
 constexpr int W_BYTES = W_TMIN + ((kLmTiles * 4 + 15) & ~15);
-constexpr int LDS_BYTES = L_SHARED_END + WAVES * W_BYTES;
+constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
+constexpr int LDS_BYTES = L_WG + 16 + 8 * WAVES;
 constexpr int kRescoreFrames = 16;
 static_assert(LDS_BYTES * kScoreWGsPerCU <= 160 * 1024, "the workgroups of a CU must fit its LDS");
 static_assert(16 % kFPP == 0, "passes must tile the 16-frame log-mel tile");
@@ -790,6 +791,164 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     EWK_TACC(3, t4, t5);
 }
 
+
+// Ring mode (few segments per tick, latency matters): the workgroup's waves share one
+// segment -- wave w takes tiles w, w + WAVES, ... -- and meet twice: for the segment's
+// log-mel max (top_db threshold) and to combine their shifted sums.  Wave w's sums are
+// shifted by its own first column (cref_w); wave 0 re-centres them on cref_0:
+//   S1 = sum_w s1_w + n_w d_w,  S2 = sum_w s2_w + 2 d_w s1_w + n_w d_w^2,  d_w = cref_w - cref_0.
+// Leaves mean / std (fp32-rounded) in misc0[0..19], misc0[20..39] (wave 0's scratch).
+template <int RING>
+__device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, float* scr, float* tile,
+                                   float* tmins, float4* gscr, int scr_tiles, int wave, int lane,
+                                   const int (&lo)[8], float* misc0) {
+    const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
+    float* wg_mm = reinterpret_cast<float*>(smem + L_WG + 16);   // [WAVES][2] max, min
+    const int T = 1 + v.len / HOP;
+    const int ntile = (T + 15) >> 4;
+    const int npass = (T + kFPP - 1) / kFPP;
+    const int nloc = ntile > wave ? (ntile - wave + WAVES - 1) / WAVES : 0;
+    const bool park = nloc <= scr_tiles;
+    const int col = lane & 15;
+    float4* gcol = gscr + (int64_t)scr_tiles * 8 * 64;
+    float4* tile4 = reinterpret_cast<float4*>(tile);
+    double s1[8], s2[8];
+    float cref[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
+    float vmax = -INFINITY, vmin = INFINITY;
+    auto run_tile = [&](int tile_i, float& mx, float& mn) {
+        {   // stage the tile's first pass
+            float r[kStageLoads];
+            stage_load(v, tile_i * 16 * HOP - NFFT / 2, lane, r);
+            stage_store(scr, lane, r);
+            lds_order();
+        }
+#pragma unroll 1
+        for (int p = 0; p < 16 / kFPP; ++p) {
+            const int pass = tile_i * (16 / kFPP) + p;
+            if (pass < npass)
+                frame_pass(v, pass * kFPP, T, p * kFPP, p + 1 < 16 / kFPP && pass + 1 < npass, smem, scr, tile, lane,
+                           lo, mx, mn);
+            else
+                zero_rows(tile, p * kFPP, lane);
+        }
+        lds_order();
+    };
+    for (int lt = 0; lt < nloc; ++lt) {
+        const int tile_i = wave + WAVES * lt;
+        float tmin = INFINITY;
+        run_tile(tile_i, vmax, tmin);
+        if (park) {
+            float4* dst = gscr + (int64_t)lt * 8 * 64 + lane;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) dst[k * 64] = tile4[k * 64 + lane];
+        }
+        float c[8];
+        tile_dct(tile, s_dct, lane, c);
+        if (lt == 0) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
+        }
+        stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
+        if (park) {
+            float4* dst = gcol + (int64_t)lt * 2 * 64 + lane;
+            dst[0] = make_float4(c[0], c[1], c[2], c[3]);
+            dst[64] = make_float4(c[4], c[5], c[6], c[7]);
+        }
+        vmin = fminf(vmin, tmin);
+        tmin = wave_min(tmin);
+        if (lane == 0) tmins[lt] = tmin;
+    }
+    vmax = wave_max(vmax);
+    vmin = wave_min(vmin);
+    if (lane == 0) { wg_mm[2 * wave] = vmax; wg_mm[2 * wave + 1] = vmin; }
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) { vmax = fmaxf(vmax, wg_mm[2 * w]); vmin = fminf(vmin, wg_mm[2 * w + 1]); }
+    const float theta = vmax - 80.0f;
+    if (vmin < theta && nloc > 0) {
+        lds_order();
+        if (park) {
+            for (int lt = 0; lt < nloc; ++lt) {
+                if (!(tmins[lt] < theta)) continue;
+                const int tile_i = wave + WAVES * lt;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const float4 x = gscr[(int64_t)lt * 512 + k * 64 + lane];
+                    tile4[k * 64 + lane] = make_float4(fmaxf(x.x, theta), fmaxf(x.y, theta), fmaxf(x.z, theta),
+                                                       fmaxf(x.w, theta));
+                }
+                const float4 o0 = gcol[(int64_t)lt * 128 + lane], o1 = gcol[(int64_t)lt * 128 + 64 + lane];
+                const float co[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
+                lds_order();
+                float cn[8];
+                tile_dct(tile, s_dct, lane, cn);
+                stats_replace(cn, co, cref, tile_i * 16 + col < T, s1, s2);
+            }
+        } else {   // more tiles than the scratch holds: recompute them with the clamp
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; }
+            for (int lt = 0; lt < nloc; ++lt) {
+                const int tile_i = wave + WAVES * lt;
+                float d0 = 0.f, d1 = 0.f;
+                run_tile(tile_i, d0, d1);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const float4 x = tile4[k * 64 + lane];
+                    tile4[k * 64 + lane] = make_float4(fmaxf(x.x, theta), fmaxf(x.y, theta), fmaxf(x.z, theta),
+                                                       fmaxf(x.w, theta));
+                }
+                lds_order();
+                float c[8];
+                tile_dct(tile, s_dct, lane, c);
+                stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
+            }
+        }
+    }
+    // this wave's per-coefficient (s1, s2, cref) -> its scratch, as doubles [coef][3]
+    double* pd = reinterpret_cast<double*>(scr);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { s1[i] = row_sum_d(s1[i]); s2[i] = row_sum_d(s2[i]); }
+    if (col == 15) {
+        const int h = lane >> 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int k = 4 * h + r;
+            pd[3 * k] = s1[r]; pd[3 * k + 1] = s2[r]; pd[3 * k + 2] = (double)cref[r];
+            if (h == 0) {
+                const int k2 = 16 + r;
+                pd[3 * k2] = s1[4 + r]; pd[3 * k2 + 1] = s2[4 + r]; pd[3 * k2 + 2] = (double)cref[4 + r];
+            }
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        double mean = 0.0, sd = 0.0;
+        if (lane < NMFCC) {
+            const double* p0 = reinterpret_cast<const double*>(smem + L_SHARED_END + W_SCR);
+            const double r0 = p0[3 * lane + 2];
+            double S1 = 0.0, S2 = 0.0;
+            for (int w = 0; w < WAVES; ++w) {
+                int n = 0;   // valid frames of wave w's tiles
+                for (int ti = w; ti < ntile; ti += WAVES) n += min(16, T - 16 * ti);
+                if (n == 0) continue;
+                const double* pw = reinterpret_cast<const double*>(smem + L_SHARED_END + w * W_BYTES + W_SCR);
+                const double a1 = pw[3 * lane], a2 = pw[3 * lane + 1], d = pw[3 * lane + 2] - r0;
+                S1 += a1 + (double)n * d;
+                S2 += a2 + 2.0 * d * a1 + (double)n * d * d;
+            }
+            const double Td = (double)T;
+            mean = r0 + S1 / Td;
+            double var = (S2 - S1 * S1 / Td) / Td;
+            sd = sqrt(var > 0.0 ? var : 0.0);
+        }
+        lds_order();
+        if (lane < NMFCC) { misc0[lane] = (float)mean; misc0[20 + lane] = (float)sd; }
+        lds_order();
+    }
+}
+
 // ---- the score, exactly as WordMatcher.calculate_similarity evaluates it --------
 // (wakeword.py:611-625 with scipy 1.15 `correlation`: dist = clip(1 - uv/sqrt(uu*vv), 0, 2)).
 // The template u is float32 (librosa.load -> float32 MFCCs).  numpy's dot of two
@@ -885,6 +1044,43 @@ __device__ __forceinline__ double score_f32_finish(float uu_m, float uu_s, float
     return (double)(powf(percent, 1.5f) / 10.0f);
 }
 
+// Score one segment from its fp32-rounded mean / std in misc[0..39] (one wave):
+// wave-parallel dots in a fixed butterfly order, lane 0 finishes the score, writes the
+// decision and queues the segment for the fp64 re-score when it is near the threshold.
+template <int RING>
+__device__ __forceinline__ void score_epilogue(const ScoreArgs& a, const float* misc, float tmf, float tsf, bool act,
+                                               int lane, int seg, int len) {
+    const float cmf = act ? misc[lane] : 0.0f, csf = act ? misc[20 + lane] : 0.0f;
+    double score;
+    if (a.cand_f32) {   // float32 candidates: float products, float-rounded dots (sdot)
+        const float uv_m = (float)wave_sum_d((double)(tmf * cmf)), vv_m = (float)wave_sum_d((double)(cmf * cmf));
+        const float uv_s = (float)wave_sum_d((double)(tsf * csf)), vv_s = (float)wave_sum_d((double)(csf * csf));
+        score = score_f32_finish(a.uu_m32, a.uu_s32, uv_m, vv_m, uv_s, vv_s);
+    } else {
+        const double uv_m = wave_sum_d((double)tmf * (double)cmf), vv_m = wave_sum_d((double)cmf * (double)cmf);
+        const double uv_s = wave_sum_d((double)tsf * (double)csf), vv_s = wave_sum_d((double)csf * (double)csf);
+        score = score_f64_finish((double)a.uu_m32, (double)a.uu_s32, uv_m, vv_m, uv_s, vv_s);
+    }
+    if (lane == 0) {
+        const int match = score >= a.threshold;
+        // fp64 re-score: decisions within the margin of the threshold, and very short
+        // segments (T <= kRescoreFrames) whose 2..16-frame std vectors are too
+        // ill-conditioned for the float32 pipeline to meet 1e-4.
+        const bool near = fabs(score - a.threshold) < a.rescore_margin || (1 + len / HOP) <= kRescoreFrames;
+        if (RING) {
+            a.events[seg].score = score;
+            a.events[seg].match = match;
+        } else {
+            a.out_score[seg] = score;
+            if (a.out_match) a.out_match[seg] = (uint8_t)match;
+        }
+        if (near && a.rescore_list) {
+            const int slot = atomicAdd(a.rescore_count, 1);
+            if (slot < a.rescore_cap) a.rescore_list[slot] = seg;
+        }
+    }
+}
+
 template <int RING>
 __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const Tables* __restrict__ tab, ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -955,6 +1151,25 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
     const bool act = lane < NMFCC;
     const float tmf = (a.has_template && act) ? a.tmpl[lane] : 0.0f;
     const float tsf = (a.has_template && act) ? a.tmpl[NMFCC + lane] : 0.0f;
+    if (RING) {   // one segment per workgroup at a time, its tiles spread over the waves
+        int* wg_idx = reinterpret_cast<int*>(smem + L_WG);
+        float* misc0 = reinterpret_cast<float*>(smem + L_SHARED_END + W_MISC);
+        for (;;) {
+            if (threadIdx.x == 0) wg_idx[0] = atomicAdd(a.work, 1);
+            __syncthreads();
+            const int idx = wg_idx[0];
+            __syncthreads();
+            if (idx >= count) break;
+            const int seg = base + idx;
+            const ewk_event ev = a.events[seg];
+            if (ev.flags & EWK_EV_SKIPPED) continue;
+            const SegSrc<RING> v = make_src<RING>(a.pcm + (int64_t)ev.stream * a.ring_len, ev.ring_start,
+                                                  a.ring_len, ev.length);
+            segment_stats_coop(v, smem, scr, tile, tmins, gscr, a.lm_tiles, wave, lane, lo, misc0);
+            if (wave == 0 && a.has_template) score_epilogue<RING>(a, misc0, tmf, tsf, act, lane, seg, v.len);
+        }
+        return;
+    }
     for (;;) {
         EWK_TS(ta);
         int idx = 0;
@@ -1004,38 +1219,7 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
             if (a.out_mean) a.out_mean[(int64_t)seg * NMFCC + lane] = misc[lane];
             if (a.out_std) a.out_std[(int64_t)seg * NMFCC + lane] = misc[20 + lane];
         }
-        if (a.has_template) {
-            // wave-parallel dots (fixed butterfly order), lane 0 finishes the score
-            const float cmf = act ? misc[lane] : 0.0f, csf = act ? misc[20 + lane] : 0.0f;
-            double score;
-            if (a.cand_f32) {   // float32 candidates: float products, float-rounded dots (sdot)
-                const float uv_m = (float)wave_sum_d((double)(tmf * cmf)), vv_m = (float)wave_sum_d((double)(cmf * cmf));
-                const float uv_s = (float)wave_sum_d((double)(tsf * csf)), vv_s = (float)wave_sum_d((double)(csf * csf));
-                score = score_f32_finish(a.uu_m32, a.uu_s32, uv_m, vv_m, uv_s, vv_s);
-            } else {
-                const double uv_m = wave_sum_d((double)tmf * (double)cmf), vv_m = wave_sum_d((double)cmf * (double)cmf);
-                const double uv_s = wave_sum_d((double)tsf * (double)csf), vv_s = wave_sum_d((double)csf * (double)csf);
-                score = score_f64_finish((double)a.uu_m32, (double)a.uu_s32, uv_m, vv_m, uv_s, vv_s);
-            }
-            if (lane == 0) {
-            const int match = score >= a.threshold;
-            // fp64 re-score: decisions within the margin of the threshold, and very
-            // short segments (T <= kRescoreFrames) whose 2..16-frame std vectors are
-            // too ill-conditioned for the float32 pipeline to meet 1e-4.
-            const bool near = fabs(score - a.threshold) < a.rescore_margin || (1 + v.len / HOP) <= kRescoreFrames;
-            if (RING) {
-                a.events[seg].score = score;
-                a.events[seg].match = match;
-            } else {
-                a.out_score[seg] = score;
-                if (a.out_match) a.out_match[seg] = (uint8_t)match;
-            }
-            if (near && a.rescore_list) {
-                const int slot = atomicAdd(a.rescore_count, 1);
-                if (slot < a.rescore_cap) a.rescore_list[slot] = seg;
-            }
-            }
-        }
+        if (a.has_template) score_epilogue<RING>(a, misc, tmf, tsf, act, lane, seg, v.len);
         lds_order();
         EWK_TS(td);
         EWK_TACC(5, tc, td);
@@ -1186,6 +1370,10 @@ __global__ __launch_bounds__(256) void k_score_f64(const Tables64* __restrict__ 
     __shared__ double s_red[4];
     __shared__ double s_stat[2 * NMFCC];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    int count;
+    if (a.rescore_list) count = min(*a.rescore_count, a.rescore_cap);
+    else count = RING ? min(a.n_seg, *a.n_events) : a.n_seg;
+    if ((int)blockIdx.x >= count) return;   // nothing for this workgroup (the common case per tick)
     for (int i = tid; i < NFFT; i += 256) s_win[i] = tb->win[i];
     for (int i = tid; i < 128; i += 256) s_tw[i] = make_double2(tb->cs[2 * i], -tb->sn[2 * i]);   // W256^i = W512^2i
     for (int i = tid; i < NBIN; i += 256) s_cs[i] = make_double2(tb->cs[i], tb->sn[i]);
@@ -1194,9 +1382,6 @@ __global__ __launch_bounds__(256) void k_score_f64(const Tables64* __restrict__ 
     for (int i = tid; i < NMEL; i += 256) s_mlo[i] = tb->mel_lo[i];
     for (int i = tid; i <= NMEL; i += 256) s_moff[i] = tb->mel_off[i];
     __syncthreads();
-    int count;
-    if (a.rescore_list) count = min(*a.rescore_count, a.rescore_cap);
-    else count = RING ? min(a.n_seg, *a.n_events) : a.n_seg;
     double* lm = scratch + (int64_t)blockIdx.x * per_seg;   // [T][128] log-mel, then [T][20] mfcc
     double2* z = s_z[wave];
     double* pw = s_p[wave];
