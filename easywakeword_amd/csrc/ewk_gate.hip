@@ -36,6 +36,9 @@
 // float64 parity with numpy requires un-fused multiply/add (e.g. the percentile lerp)
 #pragma clang fp contract(off)
 
+#ifndef EWK_GATE_NT
+#define EWK_GATE_NT 1   // 1: non-temporal tick loads (read once; measured -6%), 2: also non-temporal ring stores (no gain)
+#endif
 #ifndef EWK_GATE_TIMING
 #define EWK_GATE_TIMING 0   // per-phase s_memtime accounting (scripts/mb_gate.py variants only)
 #endif
@@ -400,7 +403,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
 #pragma unroll
         for (int m = 0; m < kIngestLoads; ++m) {
             const int i = c0 + lane + 64 * m;
+#if EWK_GATE_NT
+            xin[m] = i < fs ? (g.pcm16 ? (float)__builtin_nontemporal_load(g.pcm16 + so + i) * (1.0f / 32768.0f)
+                                       : __builtin_nontemporal_load(g.pcm + so + i)) : 0.0f;
+#else
             xin[m] = i < fs ? (g.pcm16 ? (float)g.pcm16[so + i] * (1.0f / 32768.0f) : g.pcm[so + i]) : 0.0f;
+#endif
         }
     };
     load_chunk(0, 0);
@@ -453,7 +461,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
                 if (i < fs) {
                     int k = p0 + i;
                     if (k >= R) k -= R;
+#if EWK_GATE_NT & 2
+                    __builtin_nontemporal_store(xin[m], ring + k);
+#else
                     ring[k] = xin[m];
+#endif
                     if (staged) stage[i] = xin[m];
                 }
             }
