@@ -154,3 +154,48 @@ def test_lagged_poll_pipelines_one_call_behind():
     for k, ev in enumerate(blocking):
         np.testing.assert_array_equal(lagged[k + 1], ev)
     assert sum(len(e) for e in blocking) >= 8
+
+
+def test_long_segments_cooperative_scorer(template):
+    """Segments of 8 s and 26 s through the ring-mode scorer: a workgroup's waves
+    share each segment (7 and 21 tiles per wave: the parked top_db pass and the
+    recompute fallback for more tiles than the per-wave scratch holds), scores
+    vs the oracle."""
+    gate = dict(pre_speech_silence=0.8, speech_duration_min=0.3, speech_duration_max=40.0,
+                post_speech_silence=0.4, buffer_seconds=60)
+    sr = 16000
+    streams = []
+    for i, dur in enumerate((26.0, 8.0)):
+        rng = np.random.default_rng(70 + i)
+        n = int(90.0 * sr)   # the gate starts once the 60 s ring is full
+        x = (rng.standard_normal(n) * 1e-4).astype(np.float64)
+        a, b = int(61.5 * sr), int((61.5 + dur) * sr)
+        t = np.arange(b - a) / sr
+        x[a:b] += 0.3 * np.sin(2 * np.pi * (440.0 + 60 * i) * t) * (1.0 + 0.3 * np.sin(2 * np.pi * 0.7 * t))
+        streams.append(x.astype(np.float32))
+    L = min(len(s) for s in streams)
+    L -= L % 1600
+    data = np.stack([s[:L] for s in streams])
+    eng = _engine(2, gate, max_segment_seconds=40.0)
+    eng.set_template(*template)
+    got = []
+    step = 16 * 1600
+    for c in range(0, L, step):
+        eng.push_many(data[:, c:c + step])
+        got.extend(eng.poll().tolist())
+    tm, ts = template
+    cfg = GateConfig(pre_speech_silence=0.8, speech_duration_min=0.3, speech_duration_max=40.0,
+                     post_speech_silence=0.4, buffer_seconds=60, max_segment_seconds=40.0)
+    n_long = 0
+    for i in range(2):
+        ref = run_stream(data[i], cfg).events
+        mine = sorted([g for g in got if g[0] == i], key=lambda g: g[2])
+        assert [(g[2], g[1], bool(g[7] & 1)) for g in mine] == [(e.tick, e.length, e.skipped) for e in ref], i
+        for g, e in zip(mine, ref):
+            if e.skipped:
+                continue
+            cm, cs = mfcc_ref.extract_mfcc(e.audio)
+            s = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
+            assert score_close(g[5], s, 1e-4), (i, g[1], g[5], s)
+            n_long += e.length > 7 * sr
+    assert n_long == 2

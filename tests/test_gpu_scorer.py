@@ -145,7 +145,7 @@ def test_edge_lengths(engine):
     engine.template_from_pcm(synth.load_word())
     tm, ts = engine.get_template()
     segs = [np.full(n, 0.1, np.float32) * np.sin(np.arange(n, dtype=np.float32)) for n in
-            (1, 2, 159, 160, 161, 255, 256, 257, 511, 512, 513, 2559, 2560, 2561, 48000, 48161)]
+            (1, 2, 159, 160, 161, 255, 256, 257, 511, 512, 513, 2559, 2560, 2561, 48000, 48161, 60000, 100003)]
     _, _, score, _ = engine.score(segs, candidate_dtype="float64")
     for i, x in enumerate(segs):
         cm, cs = mfcc_ref.extract_mfcc(x.astype(np.float64))
