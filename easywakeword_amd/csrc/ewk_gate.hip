@@ -265,9 +265,9 @@ __device__ __forceinline__ double percentile25_sorted(const double* sorted, int 
 }
 
 #ifndef EWK_GATE_WPE
-#define EWK_GATE_WPE 4
+#define EWK_GATE_WPE 2   // min waves per SIMD the register allocator must allow (4 spills: measured slower)
 #endif
-constexpr int kIngestLoads = 16;   // tick samples per lane loaded before the ring stores
+constexpr int kIngestLoads = 4;    // tick samples per lane loaded ahead of the ring stores (16: 166 VGPRs, 3 waves/SIMD, 10 % slower)
 
 // ---- register-resident block RMS multiset (n_blocks <= 64 * RB) ------------------
 // Element i of a per-stream array lives in lane i % 64, slot i / 64.

@@ -705,7 +705,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         }
         vmin = fminf(vmin, tmin);
         tmin = wave_min(tmin);
-        if (lane == 0) tmins[tile_i] = tmin;
+        if (lane == 0) tmins[min(tile_i, kLmTiles - 1)] = tmin;   // kLmTiles slots: only the parked path reads them
         EWK_TS(t2);
         EWK_TACC(1, t1, t2);
     }
@@ -858,7 +858,7 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
         }
         vmin = fminf(vmin, tmin);
         tmin = wave_min(tmin);
-        if (lane == 0) tmins[lt] = tmin;
+        if (lane == 0) tmins[min(lt, kLmTiles - 1)] = tmin;
     }
     vmax = wave_max(vmax);
     vmin = wave_min(vmin);
