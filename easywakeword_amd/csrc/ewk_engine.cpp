@@ -81,6 +81,7 @@ struct ewk_engine {
     DevBuf<int32_t> rescore_buf;    // [0] = count, [1..] list
     int32_t* d_rescore = nullptr;   // == rescore_buf.p
     int32_t* d_work = nullptr;      // scorer work counter
+    DevBuf<int32_t> order;          // linear batches: longest-first work order (k_lpt_order)
     int32_t rescore_cap = 4096;
     DevBuf<double> f64_scratch;
     DevBuf<float2> lm_scratch;      // parked log-mel tiles + their DCT columns, kLmTiles x 10 KB per scorer wave
@@ -191,6 +192,8 @@ static hipError_t reserve_rescore(ewk_engine* e, int32_t n_seg) {
     err = e->rescore_buf.reserve((size_t)n_seg + 1);
     if (err != hipSuccess) return err;
     e->d_rescore = e->rescore_buf.p;
+    err = e->order.reserve((size_t)n_seg);
+    if (err != hipSuccess) return err;
     e->rescore_cap = n_seg;
     return hipSuccess;
 }
@@ -248,6 +251,7 @@ void ewk_destroy(ewk_engine* e) {
     (void)hipFree(e->d_work);
     e->f64_scratch.release();
     e->lm_scratch.release();
+    e->order.release();
     e->pcm.release();
     e->offsets.release();
     e->lengths.release();
@@ -471,6 +475,7 @@ static ScoreArgs base_args(ewk_engine* e) {
     a.work = e->d_work;
     a.lm_scratch = e->lm_scratch.p;
     a.lm_tiles = kLmTiles;
+    a.order = e->order.p;
     return a;
 }
 

@@ -91,6 +91,7 @@ struct ScoreArgs {
     int32_t rescore_cap;
     float2* lm_scratch;       // per-wave parked log-mel tiles for the top_db clamp pass
     int32_t lm_tiles;         // tiles per wave in lm_scratch
+    int32_t* order;           // linear mode: work order scratch [n_seg] (longest first), nullptr = index order
 };
 
 hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mode, hipStream_t s);

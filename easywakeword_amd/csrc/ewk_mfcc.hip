@@ -501,12 +501,18 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
         const int jx = j ^ (sw & 15), sb = sw >> 4;
         float* re = tile + r * NMEL + jx + 16 * sb;   // even i: column 16*(i+sb) + jx
         float* ro = tile + r * NMEL + jx - 16 * sb;   // odd  i: column 16*(i-sb) + jx
+        // Rows of frames past T keep their (finite: silence gives -100 dB) values: the
+        // DCT columns are independent and the statistics skip those frames, so only
+        // the frame's max/min needs the validity test, once per frame.
+        float fmx = db[g][0], fmn = db[g][0];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            vmax = fmaxf(vmax, valid[g] ? db[g][i] : -INFINITY);
-            vmin = fminf(vmin, valid[g] ? db[g][i] : INFINITY);
-            ((i & 1) ? ro : re)[16 * i] = valid[g] ? db[g][i] : 0.0f;
+            fmx = fmaxf(fmx, db[g][i]);
+            fmn = fminf(fmn, db[g][i]);
+            ((i & 1) ? ro : re)[16 * i] = db[g][i];
         }
+        vmax = fmaxf(vmax, valid[g] ? fmx : -INFINITY);
+        vmin = fminf(vmin, valid[g] ? fmn : INFINITY);
     }
     lds_order();
     EWK_TS(p8);
@@ -1176,7 +1182,7 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
         if (lane == 0) idx = atomicAdd(a.work, 1);
         idx = __shfl(idx, 0, 64);
         if (idx >= count) break;
-        const int seg = base + idx;
+        const int seg = base + ((!RING && a.order) ? a.order[idx] : idx);
 
         int64_t start, ring = 0;
         const float* p;
@@ -1257,6 +1263,45 @@ hipError_t launch_snapshot(const int32_t* src, int32_t* dst, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Longest-first work order for a linear batch (LPT: the persistent waves' last
+// segments are the shortest, so the grid drains evenly).  One workgroup: per-wave
+// histograms of the segment's pass count (64 buckets, longest first), an exclusive
+// scan, then a scatter of the indices.  The order within a bucket is arbitrary; each
+// segment's result does not depend on it.
+constexpr int kLptBuckets = 64;
+constexpr int kLptWaves = 16;
+__global__ __launch_bounds__(64 * kLptWaves) void k_lpt_order(const int32_t* __restrict__ lengths, int32_t n,
+                                                               int32_t* __restrict__ order) {
+    __shared__ int hist[kLptWaves][kLptBuckets];
+    const int w = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < kLptWaves * kLptBuckets; i += blockDim.x) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    auto bucket = [](int32_t len) {
+        const int np = (1 + max(len, 0) / HOP + kFPP - 1) / kFPP;
+        return kLptBuckets - 1 - min(np, kLptBuckets - 1);
+    };
+    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[w][bucket(lengths[i])], 1);
+    __syncthreads();
+    if (threadIdx.x < kLptBuckets) {   // bucket-major, wave-minor exclusive scan (one wave, lane = bucket)
+        const int b = threadIdx.x;
+        int tot = 0;
+        for (int ww = 0; ww < kLptWaves; ++ww) tot += hist[ww][b];
+        int incl = tot;
+        for (int d = 1; d < kLptBuckets; d <<= 1) {
+            const int t = __shfl_up(incl, d, 64);
+            if (b >= d) incl += t;
+        }
+        int run = incl - tot;
+        for (int ww = 0; ww < kLptWaves; ++ww) {
+            const int c = hist[ww][b];
+            hist[ww][b] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) order[atomicAdd(&hist[w][bucket(lengths[i])], 1)] = i;
+}
+
 int score_grid(int n_seg, int ring_mode) {
     return ring_mode ? kScoreGridRing : max(1, min((n_seg + WAVES - 1) / WAVES, kScoreGridMax));
 }
@@ -1268,10 +1313,17 @@ hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mo
         hipError_t e = hipMemsetAsync(a.work, 0, sizeof(int32_t), s);
         if (e != hipSuccess) return e;
     }
-    if (ring_mode)
+    if (ring_mode) {
         hipLaunchKernelGGL(k_score_f32<1>, dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
-    else
-        hipLaunchKernelGGL(k_score_f32<0>, dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
+    } else {
+        ScoreArgs b = a;
+        // the order only matters once the waves queue several segments each
+        if (a.order && a.n_seg > 2 * grid * WAVES)
+            hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(64 * kLptWaves), 0, s, a.lengths, a.n_seg, a.order);
+        else
+            b.order = nullptr;
+        hipLaunchKernelGGL(k_score_f32<0>, dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, b);
+    }
     return hipGetLastError();
 }
 

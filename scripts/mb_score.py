@@ -12,6 +12,9 @@ reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 dev = torch.device("cuda", 0)
 word = bench.load_word()
 pcm, off, ln, frames, lengths, offsets = bench.make_segments(torch, dev, n, 1234, word)
+if os.environ.get("EWK_SORT"):   # experiment: hand the kernel its work longest-first (LPT)
+    order = torch.argsort(ln, descending=True)
+    off, ln = off[order].contiguous(), ln[order].contiguous()
 mean = torch.empty((n, 20), device=dev); std = torch.empty((n, 20), device=dev)
 score = torch.empty(n, device=dev, dtype=torch.float64); match = torch.empty(n, device=dev, dtype=torch.uint8)
 e = ewa.Engine()

@@ -151,3 +151,21 @@ def test_edge_lengths(engine):
         cm, cs = mfcc_ref.extract_mfcc(x.astype(np.float64))
         ref = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
         assert score_close(score[i], ref, SCORE_TOL), (len(x), score[i], ref)
+
+
+def test_longest_first_order_is_bit_identical(engine):
+    """Batches with more segments than 2 x the resident waves are handed out longest
+    first (k_lpt_order); every output must equal the index-order result of small
+    batches, bit for bit (each segment is scored by one wave, independently)."""
+    engine.template_from_pcm(synth.load_word())
+    rng = np.random.Generator(np.random.PCG64(77))
+    segs = [rng.normal(0, 0.01, int(n)).astype(np.float32) for n in rng.integers(200, 40000, 4500)]
+    segs += [np.zeros(0, np.float32), np.zeros(100, np.float32)] + [synth.load_word()] * 10
+    m1, s1, sc1, mt1 = engine.score(segs, candidate_dtype="float64")     # > 4096 segments: LPT order
+    parts = [engine.score(segs[i:i + 1500], candidate_dtype="float64") for i in range(0, len(segs), 1500)]
+    m2 = np.concatenate([p[0] for p in parts]); s2 = np.concatenate([p[1] for p in parts])
+    sc2 = np.concatenate([p[2] for p in parts]); mt2 = np.concatenate([p[3] for p in parts])
+    np.testing.assert_array_equal(m1, m2)
+    np.testing.assert_array_equal(s1, s2)
+    np.testing.assert_array_equal(sc1, sc2)     # NaN == NaN in assert_array_equal
+    np.testing.assert_array_equal(mt1, mt2)
