@@ -40,6 +40,9 @@ sys.path.insert(0, ROOT)
 
 METRIC = "real-time 16 kHz streams sustained + MFCC frames/sec at 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# VALU issue peak: 256 CUs x 4 SIMD-32 x one wave64 instruction per 2 cycles at the 2.4 GHz
+# spec clock (= the 157.3 TF FP32 vector peak counted in FMAs; MI355X_MICROARCH.md)
+VALU_PEAK_WAVE_INSTR_S = 256 * 4 * 2.4e9 / 2
 BYTES_PER_FRAME = 640          # 160 new fp32 samples per MFCC frame
 HOP = 160
 SR = 16000
@@ -464,13 +467,22 @@ def main():
         if args.fixed_len > 0 and world == 1 else None
     kernel_s = (k_ms / max(1, k_n)) / 1e3
     achieved = frames * BYTES_PER_FRAME / kernel_s / 1e9
-    traffic, traffic_src = None, None
+    traffic, traffic_src, compute = None, None, None
     tf = os.path.join(ROOT, "profiles", "traffic_k_score_f32.json")
     if os.path.exists(tf):   # PMC-measured HBM bytes/frame of this kernel (scripts/gpu_round.sh pmc)
         with open(tf) as fh:
             t = json.load(fh)
         traffic = t["traffic_bytes_per_frame"] * frames / 1e9
         traffic_src = f"profiles/traffic_k_score_f32.json ({t['segments']} segments, {t['method']})"
+        if t.get("valu_instr_per_frame"):
+            # the bound that actually binds k_score_f32: VALU issue
+            ach = t["valu_instr_per_frame"] * frames / kernel_s
+            compute = {"bound": "valu-issue", "achieved": ach / 1e12, "peak": VALU_PEAK_WAVE_INSTR_S / 1e12,
+                       "unit": "T wave64-instr/s", "frac": ach / VALU_PEAK_WAVE_INSTR_S,
+                       "valu_instr_per_frame": t["valu_instr_per_frame"],
+                       "frames_per_s_at_valu_peak": VALU_PEAK_WAVE_INSTR_S / t["valu_instr_per_frame"],
+                       "source": "SQ_INSTS_VALU per frame from profiles/traffic_k_score_f32.json x frames / "
+                                 "HIP-event kernel time; peak at the 2.4 GHz spec clock"}
 
     out = {
         "metric": METRIC,
@@ -507,6 +519,7 @@ def main():
             "launches": k_n,
             "algorithmic_bytes_per_launch": frames * BYTES_PER_FRAME,
         },
+        "compute_roofline": compute,
         "step_event_ms": step_ms,
         "rescore_kernel_ms": r_ms / max(1, r_n),
         "matches_per_step": n_match,

@@ -17,6 +17,10 @@ SOURCES = ["ewk_mfcc.hip", "ewk_gate.hip", "ewk_level3.hip", "ewk_engine.cpp", "
 HEADERS = ["ewk_internal.h", "ewk_gate.h", os.path.join("..", "..", "include", "ewk.h")]
 LIB = os.path.join(HERE, "libewk.so")
 ARCH = os.environ.get("EWK_OFFLOAD_ARCH", "gfx950")
+# Per-source flags.  The scorer is VALU-issue bound: SLP-packed f32 ops (v_pk_add_f32)
+# cost more issue slots than the two scalar ops they replace on gfx950 and force
+# register-pair moves (-3.3 % k_score_f32 time without them).
+EXTRA = {"ewk_mfcc.hip": ["-fno-slp-vectorize"]}
 
 
 def _hipcc() -> str:
@@ -44,7 +48,8 @@ def build(force: bool = False, verbose: bool = False, out: str = None, defines=(
         obj = os.path.join(CSRC, src.rsplit(".", 1)[0] + ".o")
         obj = obj + "".join(f".{d}" for d in defines).replace("=", "_")
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-               "-Wno-unused-function"] + [f"-D{d}" for d in defines] + ["-c", os.path.join(CSRC, src), "-o", obj]
+               "-Wno-unused-function"] + EXTRA.get(src, []) + [f"-D{d}" for d in defines] + \
+            ["-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

@@ -12,7 +12,8 @@ for f in easywakeword_amd/csrc/ewk_mfcc.hip easywakeword_amd/csrc/ewk_gate.hip e
 done
 objs=""
 for s in ewk_mfcc.hip ewk_gate.hip ewk_level3.hip ewk_engine.cpp ewk_tables.cpp; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function "$@" \
+  x=""; [ "$s" = ewk_mfcc.hip ] && x="-fno-slp-vectorize"   # as easywakeword_amd/build.py EXTRA
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function $x "$@" \
      -c "$T/easywakeword_amd/csrc/$s" -o "$T/$s.o" &
   objs="$objs $T/$s.o"
 done

@@ -83,8 +83,12 @@ def main():
                 json.dump({"kernel": "k_score_f32", "segments": n, "frames": frames,
                            "fetch_bytes": fetch, "write_bytes": write, "traffic_bytes": fetch + write,
                            "traffic_bytes_per_frame": (fetch + write) / frames,
-                           "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE, separate passes, "
-                                     "median over dispatches of scripts/mb_score.py"}, fh, indent=1)
+                           # wave-instructions per MFCC frame (bench.py's VALU-issue roofline)
+                           "valu_instr_per_frame": c.get("SQ_INSTS_VALU", 0.0) / frames,
+                           "lds_instr_per_frame": c.get("SQ_INSTS_LDS", 0.0) / frames,
+                           "mfma_instr_per_frame": c.get("SQ_INSTS_MFMA", 0.0) / frames,
+                           "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE, SQ_INSTS_* "
+                                     "in separate passes, median over dispatches of scripts/mb_score.py"}, fh, indent=1)
 
 
 if __name__ == "__main__":
