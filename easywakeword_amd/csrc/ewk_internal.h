@@ -17,7 +17,6 @@ constexpr int NBIN = NFFT / 2 + 1;   // 257
 constexpr int NMEL = 128;
 constexpr int NMFCC = EWK_N_MFCC;    // 20
 constexpr int MEL_ITERS = 40;        // unrolled mel FMAs per lane: sum of per-group band widths
-constexpr int DCT_PITCH = 130;       // LDS row pitch of the DCT table (bank-conflict free A reads)
 constexpr int SCR_FRAME = 272;       // per-frame FFT scratch floats (16 rows x 17)
 // fp32 scorer shape: frames per 16-lane group per pass (kNF), waves per workgroup and
 // workgroups per CU.  kNF = 2 doubles the per-wave FFT state (ILP) and its LDS, so the

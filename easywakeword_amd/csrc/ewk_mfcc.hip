@@ -71,7 +71,12 @@ constexpr int L_TW2 = L_TW1 + 16 * TP * 8;                // [j][k2] = tw2[j + 1
 constexpr int L_WPAD = L_TW2 + 16 * TP * 8;               // [j][kMelOff[i] + q] = wpad[16*(it0_i + q) + j]
 constexpr int L_BLO = L_WPAD + 16 * WP * 4;
 constexpr int L_DCT = L_BLO + NMEL * 4;
-constexpr int L_SHARED_END = ((L_DCT + NMFCC * DCT_PITCH * 4) + 15) & ~15;
+// DCT image for the MFMA A operand, k-major per lane: [h][row][s] = D[row][4s + h] with
+// 36-float runs (two b128 reads fetch a lane's 8 k-steps, at most 2-way bank
+// conflicts); row NMFCC is zero (the acc1 lanes past coefficient 19 read it).
+constexpr int DCT_ROWS = NMFCC + 1;
+constexpr int DCT_HP = 36;
+constexpr int L_SHARED_END = ((L_DCT + 4 * DCT_ROWS * DCT_HP * 4) + 15) & ~15;
 // Frames per wave pass: kNF per 16-lane group (kNF = 2: two independent FFTs per lane).
 constexpr int kFPP = 4 * kNF;
 constexpr int kStageLoads = ((kFPP - 1) * HOP + NFFT + 63) / 64;   // dword loads per lane per pass
@@ -92,6 +97,28 @@ static_assert(16 % kFPP == 0, "passes must tile the 16-frame log-mel tile");
 
 
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
+// Eight ds_read_b128 of consecutive 16-B chunks issued together, and their wait.
+// Written as asm so the scheduler cannot sink each read next to its first use (at
+// 256 VGPRs it does, and every read then costs a full LDS round trip).
+#define EWK_LD128(r, a, c) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[c]) : "v"(a), "i"(16 * (c)) : "memory")
+#define EWK_LD128_8(r, addr)                                                                        \
+    do {                                                                                           \
+        const uint32_t _a = (addr);                                                                \
+        EWK_LD128(r, _a, 0); EWK_LD128(r, _a, 1); EWK_LD128(r, _a, 2); EWK_LD128(r, _a, 3);         \
+        EWK_LD128(r, _a, 4); EWK_LD128(r, _a, 5); EWK_LD128(r, _a, 6); EWK_LD128(r, _a, 7);         \
+    } while (0)
+#define EWK_LD128S(r, a, c, st) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[c]) : "v"(a), "i"((st) * (c)) : "memory")
+// the 8 KB log-mel tile as float4 [8][64], lane-strided (park copies)
+#define EWK_LD_TILE(r, addr)                                                                               \
+    do {                                                                                                  \
+        const uint32_t _a = (addr);                                                                       \
+        EWK_LD128S(r, _a, 0, 1024); EWK_LD128S(r, _a, 1, 1024); EWK_LD128S(r, _a, 2, 1024); EWK_LD128S(r, _a, 3, 1024); \
+        EWK_LD128S(r, _a, 4, 1024); EWK_LD128S(r, _a, 5, 1024); EWK_LD128S(r, _a, 6, 1024); EWK_LD128S(r, _a, 7, 1024); \
+    } while (0)
+#define EWK_WAIT_8(r)                                                                              \
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), \
+                 "+v"(r[5]), "+v"(r[6]), "+v"(r[7]) : : "memory")
 
 __device__ __forceinline__ float2 cmul(float2 a, float2 w) {
     return make_float2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
@@ -243,6 +270,9 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
             EWK_LD64(8); EWK_LD64(9); EWK_LD64(10); EWK_LD64(11); EWK_LD64(12); EWK_LD64(13); EWK_LD64(14); EWK_LD64(15);
 #undef EWK_LD64
         }
+        floatx4 w4[8];   // this lane's window pairs, fetched in the same batch
+        EWK_LD128_8(w4, (uint32_t)(uintptr_t)(reinterpret_cast<const float4*>(smem + L_WIN2) + j * (TP / 2)));
+        EWK_WAIT_8(w4);
 #pragma unroll
         for (int g = 0; g < kNF; ++g)
             asm volatile("s_waitcnt lgkmcnt(0)"
@@ -251,10 +281,9 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
                            "+v"(x[g][12]), "+v"(x[g][13]), "+v"(x[g][14]), "+v"(x[g][15])
                          :
                          : "memory");
-        const float4* w4 = reinterpret_cast<const float4*>(smem + L_WIN2) + j * (TP / 2);
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-            const float4 w = w4[c];
+            const floatx4 w = w4[c];
 #pragma unroll
             for (int g = 0; g < kNF; ++g) {
                 a[g][2 * c] = make_float2(x[g][2 * c].x * w.x, x[g][2 * c].y * w.y);
@@ -271,13 +300,15 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     EWK_TS(p2);
     if (tim) EWK_TACC(9, p1, p2);
     // ---- DFT16 over n1, twiddle W256^(j*k1) (one twiddle row serves every frame of the lane)
-#pragma unroll
-    for (int g = 0; g < kNF; ++g) dft16_perm(a[g]);
     {
-        const float4* t4 = reinterpret_cast<const float4*>(smem + L_TW1) + j * (TP / 2);
+        floatx4 t4[8];   // twiddle row, requested before the DFT16s it waits behind
+        EWK_LD128_8(t4, (uint32_t)(uintptr_t)(reinterpret_cast<const float4*>(smem + L_TW1) + j * (TP / 2)));
+#pragma unroll
+        for (int g = 0; g < kNF; ++g) dft16_perm(a[g]);
+        EWK_WAIT_8(t4);
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-            const float4 w = t4[c];   // k1 = 2c+1, 2c+2
+            const floatx4 w = t4[c];   // k1 = 2c+1, 2c+2
 #pragma unroll
             for (int g = 0; g < kNF; ++g) {
                 a[g][dperm(2 * c + 1)] = cmul(a[g][dperm(2 * c + 1)], make_float2(w.x, w.y));
@@ -367,7 +398,18 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     // with itself (it = 9..16: k = 8 + 16 (it - 9)).
     {
         const bool z0 = jp == 0;
-        const float2* tw = reinterpret_cast<const float2*>(smem + L_TW2) + jp * TP;   // [j'][it], 17 entries
+        // the 17 twiddles of this lane class, fetched up front (9 ds_read_b128): read one
+        // step ahead they cost an LDS round trip per step behind that step's writes
+        float2 tw[18];
+        {
+            const float4* t4 = reinterpret_cast<const float4*>(smem + L_TW2) + jp * (TP / 2);   // [j'][it], 17 entries
+#pragma unroll
+            for (int c = 0; c < 9; ++c) {
+                const float4 q = t4[c];
+                tw[2 * c] = make_float2(q.x, q.y);
+                tw[2 * c + 1] = make_float2(q.z, q.w);
+            }
+        }
         float* pA0 = scf + rowA;                     // P[k]      at pA0[16 it]       (it <= 15)
         float* pA1 = z0 ? scf - 136 : pA0;           //           lane 0, it >= 9
         float* pA2 = z0 ? scf - 136 : pA0 - 16;      //           it = 16
@@ -525,43 +567,64 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
 
 // DCT of one 16-frame log-mel tile on the matrix cores.
 // Lane l gets C[row = 4h + r][frame col] of both row tiles (h = l>>4, col = l&15) in c[0..3], c[4..7].
+// The operands of 8 k-steps (2+2 b128 of the DCT image, 8 tile reads) are requested one
+// block ahead of the 16 MFMAs that consume them (counted lgkmcnt, 12 reads per block).
+#define EWK_DCT_LOAD(p, blk)                                                                         \
+    do {                                                                                             \
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(A0[p][0]) : "v"(a0), "i"(32 * (blk)) : "memory");      \
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(A0[p][1]) : "v"(a0), "i"(32 * (blk) + 16) : "memory"); \
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(A1[p][0]) : "v"(a1), "i"(32 * (blk)) : "memory");      \
+        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(A1[p][1]) : "v"(a1), "i"(32 * (blk) + 16) : "memory"); \
+        EWK_DCT_LB(p, blk, 0); EWK_DCT_LB(p, blk, 1); EWK_DCT_LB(p, blk, 2); EWK_DCT_LB(p, blk, 3);                 \
+        EWK_DCT_LB(p, blk, 4); EWK_DCT_LB(p, blk, 5); EWK_DCT_LB(p, blk, 6); EWK_DCT_LB(p, blk, 7);                 \
+    } while (0)
+#define EWK_DCT_LB(p, blk, u) \
+    asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(B[p][u]) : "v"(bb[u]), "i"(128 * (blk)) : "memory")
+#define EWK_DCT_WAIT(p, n)                                                                                     \
+    asm volatile("s_waitcnt lgkmcnt(" #n ")"                                                                   \
+                 : "+v"(A0[p][0]), "+v"(A0[p][1]), "+v"(A1[p][0]), "+v"(A1[p][1]), "+v"(B[p][0]), "+v"(B[p][1]), \
+                   "+v"(B[p][2]), "+v"(B[p][3]), "+v"(B[p][4]), "+v"(B[p][5]), "+v"(B[p][6]), "+v"(B[p][7])      \
+                 :                                                                                             \
+                 : "memory")
+#define EWK_DCT_MFMA(p)                                                                        \
+    _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                            \
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[p][u >> 2][u & 3], B[p][u], acc0, 0, 0, 0); \
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(A1[p][u >> 2][u & 3], B[p][u], acc1, 0, 0, 0); \
+    }
 __device__ __forceinline__ void tile_dct(const float* tile, const float* s_dct, int lane, float (&c)[8]) {
     const int col = lane & 15, h = lane >> 4;
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
     // B[k = 4s + h][col] = tile row col, band 4s + h, stored at column (4s + h) ^ swz(col);
-    // swz < 32, so bands 32u + b sit at 32u + (b ^ swz): 8 per-lane offsets + immediates.
+    // swz < 32, so bands 32u + b sit at 32u + (b ^ swz): 8 per-lane addresses + immediates.
     const int sw = tile_swz(col);
-    int boff[8];
+    const uint32_t tb = (uint32_t)(uintptr_t)tile;
+    uint32_t bb[8];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) boff[s] = col * NMEL + ((4 * s + h) ^ sw);
-    const float* arow0 = s_dct + col * DCT_PITCH + h;
-    const float* arow1 = s_dct + (16 + (col & 3)) * DCT_PITCH + h;
-    const bool a1ok = col < 4;
-#pragma unroll
-    for (int s0 = 0; s0 < 32; s0 += 8) {   // operands of 8 k-steps in flight, then 16 MFMAs
-        float bv[8], av0[8], av1[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            bv[u] = tile[boff[u] + 32 * (s0 >> 3)];
-            av0[u] = arow0[4 * (s0 + u)];
-            const float x1 = arow1[4 * (s0 + u)];
-            av1[u] = a1ok ? x1 : 0.0f;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-#if EWK_ABLATE & 16
-            acc0[u & 3] += av0[u] * bv[u];
-            acc1[u & 3] += av1[u] * bv[u];
-#else
-            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av0[u], bv[u], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av1[u], bv[u], acc1, 0, 0, 0);
-#endif
-        }
-    }
+    for (int s = 0; s < 8; ++s) bb[s] = tb + 4 * (col * NMEL + ((4 * s + h) ^ sw));
+    const uint32_t a0 = (uint32_t)(uintptr_t)(s_dct + (h * DCT_ROWS + col) * DCT_HP);
+    const uint32_t a1 = (uint32_t)(uintptr_t)(s_dct + (h * DCT_ROWS + (col < 4 ? 16 + col : NMFCC)) * DCT_HP);
+    floatx4 A0[2][2], A1[2][2];
+    float B[2][8];
+    EWK_DCT_LOAD(0, 0);
+    EWK_DCT_LOAD(1, 1);
+    EWK_DCT_WAIT(0, 12);
+    EWK_DCT_MFMA(0);
+    EWK_DCT_LOAD(0, 2);
+    EWK_DCT_WAIT(1, 12);
+    EWK_DCT_MFMA(1);
+    EWK_DCT_LOAD(1, 3);
+    EWK_DCT_WAIT(0, 12);
+    EWK_DCT_MFMA(0);
+    EWK_DCT_WAIT(1, 0);
+    EWK_DCT_MFMA(1);
     lds_order();
 #pragma unroll
     for (int i = 0; i < 4; ++i) { c[i] = acc0[i]; c[4 + i] = acc1[i]; }
 }
+#undef EWK_DCT_LOAD
+#undef EWK_DCT_LB
+#undef EWK_DCT_WAIT
+#undef EWK_DCT_MFMA
 
 // fp64 shifted sums of the frame columns that exist (d = c - cref).
 __device__ __forceinline__ void stats_add(const float (&c)[8], const float (&cref)[8], bool ok, double (&s1)[8],
@@ -692,10 +755,13 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         lds_order();
         EWK_TS(t1);
         EWK_TACC(0, t0, t1);
-        if (park) {
+        if (park) {   // all 8 reads in flight, then the stores
             float4* dst = gscr + (int64_t)tile_i * 8 * 64 + lane;
+            floatx4 t[8];
+            EWK_LD_TILE(t, (uint32_t)(uintptr_t)(tile4 + lane));
+            EWK_WAIT_8(t);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) dst[k * 64] = tile4[k * 64 + lane];
+            for (int k = 0; k < 8; ++k) dst[k * 64] = make_float4(t[k][0], t[k][1], t[k][2], t[k][3]);
         }
         float c[8];
         tile_dct(tile, s_dct, lane, c);
@@ -847,8 +913,11 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
         run_tile(tile_i, vmax, tmin);
         if (park) {
             float4* dst = gscr + (int64_t)lt * 8 * 64 + lane;
+            floatx4 t[8];
+            EWK_LD_TILE(t, (uint32_t)(uintptr_t)(tile4 + lane));
+            EWK_WAIT_8(t);
 #pragma unroll
-            for (int k = 0; k < 8; ++k) dst[k * 64] = tile4[k * 64 + lane];
+            for (int k = 0; k < 8; ++k) dst[k * 64] = make_float4(t[k][0], t[k][1], t[k][2], t[k][3]);
         }
         float c[8];
         tile_dct(tile, s_dct, lane, c);
@@ -1123,8 +1192,10 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
             sw[i] = w;
         }
         float* sd = reinterpret_cast<float*>(smem + L_DCT);
-        for (int i = threadIdx.x; i < NMFCC * NMEL; i += blockDim.x)
-            sd[(i / NMEL) * DCT_PITCH + (i % NMEL)] = tab->dct[i];
+        for (int i = threadIdx.x; i < 4 * DCT_ROWS * DCT_HP; i += blockDim.x) {
+            const int h = i / (DCT_ROWS * DCT_HP), row = (i / DCT_HP) % DCT_ROWS, k = i % DCT_HP;
+            sd[i] = (row < NMFCC && k < NMEL / 4) ? tab->dct[row * NMEL + 4 * k + h] : 0.0f;
+        }
     }
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
