@@ -695,20 +695,40 @@ __device__ __forceinline__ double wave_sum_d(double x) {
 // Wave maximum of a float (see wave_min).
 __device__ __forceinline__ float wave_max(float x) { return -wave_min(-x); }
 
-// Reduce the per-lane sums over the 16 frame columns; lane 15 of each row returns the
-// mean in s1 and the std in s2.
-__device__ __forceinline__ void finish_stats(int T, const float (&cref)[8], double (&s1)[8], double (&s2)[8]) {
+// Reduce the per-lane sums over the 16 frame columns (DPP, totals in lane 15 of each
+// row), hand each coefficient's (S1, S2, cref) to lane k = coefficient through the
+// wave's scratch `pd` (20 x 3 doubles), and finish there: lane k < 20 returns its mean in
+// s1[0] and its population std in s2[0] (one fp64 division + sqrt per lane, not eight).
+__device__ __forceinline__ void finish_stats(int T, const float (&cref)[8], double (&s1)[8], double (&s2)[8],
+                                             int lane, double* pd) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         s1[i] = row_sum_d(s1[i]);
         s2[i] = row_sum_d(s2[i]);
-        const double Td = (double)T;
-        const double mean = (double)cref[i] + s1[i] / Td;
-        double var = (s2[i] - s1[i] * s1[i] / Td) / Td;
-        var = var > 0.0 ? var : 0.0;
-        s1[i] = mean;
-        s2[i] = sqrt(var);
     }
+    if ((lane & 15) == 15) {
+        const int h = lane >> 4;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int k = 4 * h + r;
+            pd[3 * k] = s1[r]; pd[3 * k + 1] = s2[r]; pd[3 * k + 2] = (double)cref[r];
+            if (h == 0) {
+                const int k2 = 16 + r;
+                pd[3 * k2] = s1[4 + r]; pd[3 * k2 + 1] = s2[4 + r]; pd[3 * k2 + 2] = (double)cref[4 + r];
+            }
+        }
+    }
+    lds_order();
+    if (lane < NMFCC) {
+        const double S1 = pd[3 * lane], S2 = pd[3 * lane + 1], r0 = pd[3 * lane + 2];
+        const double Td = (double)T;
+        const double mean = r0 + S1 / Td;
+        double var = (S2 - S1 * S1 / Td) / Td;
+        var = var > 0.0 ? var : 0.0;
+        s1[0] = mean;
+        s2[0] = sqrt(var);
+    }
+    lds_order();
 }
 
 // Zero the kFPP tile rows of one pass (frames past T).
@@ -858,7 +878,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
 #endif
     EWK_TS(t4);
     EWK_TACC(2, t3, t4);
-    finish_stats(T, cref, s1, s2);
+    finish_stats(T, cref, s1, s2, lane, reinterpret_cast<double*>(scr));
     EWK_TS(t5);
     EWK_TACC(3, t4, t5);
 }
@@ -1119,13 +1139,12 @@ __device__ __forceinline__ double score_f32_finish(float uu_m, float uu_s, float
     return (double)(powf(percent, 1.5f) / 10.0f);
 }
 
-// Score one segment from its fp32-rounded mean / std in misc[0..39] (one wave):
+// Score one segment from its fp32-rounded mean / std (lane k < 20: coefficient k; one wave):
 // wave-parallel dots in a fixed butterfly order, lane 0 finishes the score, writes the
 // decision and queues the segment for the fp64 re-score when it is near the threshold.
 template <int RING>
-__device__ __forceinline__ void score_epilogue(const ScoreArgs& a, const float* misc, float tmf, float tsf, bool act,
+__device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, float csf, float tmf, float tsf,
                                                int lane, int seg, int len) {
-    const float cmf = act ? misc[lane] : 0.0f, csf = act ? misc[20 + lane] : 0.0f;
     double score;
     if (a.cand_f32) {   // float32 candidates: float products, float-rounded dots (sdot)
         const float uv_m = (float)wave_sum_d((double)(tmf * cmf)), vv_m = (float)wave_sum_d((double)(cmf * cmf));
@@ -1207,7 +1226,6 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
     unsigned char* wbase = smem + L_SHARED_END + wave * W_BYTES;
     float* scr = reinterpret_cast<float*>(wbase + W_SCR);
     float* tile = reinterpret_cast<float*>(wbase + W_TILE);
-    float* misc = reinterpret_cast<float*>(wbase + W_MISC);
     float4* gscr = reinterpret_cast<float4*>(a.lm_scratch) + (int64_t)(blockIdx.x * WAVES + wave) * a.lm_tiles * 10 * 64;
     float* tmins = reinterpret_cast<float*>(wbase + W_TMIN);
     int lo[8];   // first bin of this lane's bands j + 16 i
@@ -1243,7 +1261,9 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
             const SegSrc<RING> v = make_src<RING>(a.pcm + (int64_t)ev.stream * a.ring_len, ev.ring_start,
                                                   a.ring_len, ev.length);
             segment_stats_coop(v, smem, scr, tile, tmins, gscr, a.lm_tiles, wave, lane, lo, misc0);
-            if (wave == 0 && a.has_template) score_epilogue<RING>(a, misc0, tmf, tsf, act, lane, seg, v.len);
+            if (wave == 0 && a.has_template)
+                score_epilogue<RING>(a, act ? misc0[lane] : 0.0f, act ? misc0[20 + lane] : 0.0f, tmf, tsf, lane,
+                                     seg, v.len);
         }
         return;
     }
@@ -1278,25 +1298,13 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
         segment_stats(v, smem, scr, tile, tmins, gscr, a.lm_tiles, lane, lo, st1, st2, tim);
         EWK_TS(tc);
 
-        // ---- gather fp32-rounded mean/std into misc[0..19], misc[20..39]
-        if ((lane & 15) == 15) {   // finish_stats leaves each row's totals in its lane 15
-            const int h = lane >> 4;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                misc[4 * h + r] = (float)st1[r];
-                misc[20 + 4 * h + r] = (float)st2[r];
-                if (h == 0) {
-                    misc[16 + r] = (float)st1[4 + r];
-                    misc[36 + r] = (float)st2[4 + r];
-                }
-            }
+        // ---- lane k < 20 holds coefficient k's mean / std (fp32-rounded like the reference's)
+        const float cmf = act ? (float)st1[0] : 0.0f, csf = act ? (float)st2[0] : 0.0f;
+        if (act && !RING) {
+            if (a.out_mean) a.out_mean[(int64_t)seg * NMFCC + lane] = cmf;
+            if (a.out_std) a.out_std[(int64_t)seg * NMFCC + lane] = csf;
         }
-        lds_order();
-        if (lane < NMFCC && !RING) {
-            if (a.out_mean) a.out_mean[(int64_t)seg * NMFCC + lane] = misc[lane];
-            if (a.out_std) a.out_std[(int64_t)seg * NMFCC + lane] = misc[20 + lane];
-        }
-        if (a.has_template) score_epilogue<RING>(a, misc, tmf, tsf, act, lane, seg, v.len);
+        if (a.has_template) score_epilogue<RING>(a, cmf, csf, tmf, tsf, lane, seg, v.len);
         lds_order();
         EWK_TS(td);
         EWK_TACC(5, tc, td);
