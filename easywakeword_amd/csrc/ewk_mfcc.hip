@@ -322,6 +322,27 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     // Row r (16 floats) keeps column n in 4-float chunk (n>>2) ^ ((r>>2)&3): the
     // column writes (ds_write_b32, the frames of a 32-lane half 272 floats apart) and
     // the row reads (ds_read_b128) are both bank-conflict free.
+#if EWK_ABLATE & 64
+    {   // sensitivity probe: EWK_XLDS extra ds_read_b128 per pass (4 LDS cycles each)
+        floatx4 d;
+        const uint32_t da = (uint32_t)(uintptr_t)(smem + L_DCT) + 16 * j;
+#pragma unroll
+        for (int i = 0; i < EWK_XLDS; ++i) asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"(da) : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(d) : : "memory");
+        asm volatile("" : : "v"(d));
+    }
+#endif
+#if EWK_ABLATE & 128
+    {   // sensitivity probe: EWK_XVALU extra independent VALU ops per pass (4 chains)
+        float q0 = a[0][1].x, q1 = a[0][2].x, q2 = a[1][1].x, q3 = a[1][2].x;
+#pragma unroll
+        for (int i = 0; i < EWK_XVALU / 4; ++i) {
+            asm volatile("v_add_f32 %0, %0, %0" : "+v"(q0)); asm volatile("v_add_f32 %0, %0, %0" : "+v"(q1));
+            asm volatile("v_add_f32 %0, %0, %0" : "+v"(q2)); asm volatile("v_add_f32 %0, %0, %0" : "+v"(q3));
+        }
+        asm volatile("" : : "v"(q0), "v"(q1), "v"(q2), "v"(q3));
+    }
+#endif
     float2 b[kNF][16];
 #if EWK_ABLATE & 2
 #pragma unroll
