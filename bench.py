@@ -459,7 +459,10 @@ def main():
     if world > 1:
         dist.all_reduce(t_rank, op=dist.ReduceOp.MAX)
     t_max = float(t_rank.item())
-    value = frames * world * args.steps / t_max
+    frames_all = torch.tensor([frames], dtype=torch.float64, device=cdev)   # ranks' ragged batches differ
+    if world > 1:
+        dist.all_reduce(frames_all)
+    value = float(frames_all.item()) * args.steps / t_max
     n_match = int(match.sum().item())
     n_nan = int(torch.isnan(score).sum().item())
 
@@ -502,6 +505,7 @@ def main():
                         f"(L~U{{6400..33600}}), MFCC(20,512,160)+cosine match per segment",
             "segments_per_gpu": n_seg,
             "frames_per_step_per_gpu": frames,
+            "frames_per_step_all_gpus": int(frames_all.item()),
             "global_batch": n_seg * world,
             "parallelism": f"dp{world} (stream shards, RCCL all-gather of decisions)" if world > 1 else "dp1",
         },
