@@ -29,7 +29,10 @@ constexpr int kNF = EWK_NF;
 #ifndef EWK_PAIR
 #define EWK_PAIR (EWK_NF == 2)
 #endif
-constexpr int WAVES = kNF == 1 ? 4 : 8;
+#ifndef EWK_WAVES
+#define EWK_WAVES (EWK_NF == 1 ? 4 : 8)   // timing probes may shrink it (waves per SIMD)
+#endif
+constexpr int WAVES = EWK_WAVES;
 constexpr int kScoreWGsPerCU = kNF == 1 ? 2 : 1;
 
 // Host-built constant tables (ewk_tables.cpp); copied to LDS by every workgroup.
