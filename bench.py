@@ -286,12 +286,10 @@ def fixed_length_bench(torch, dev, ewa, eng, word, n_seg, seed, sh, fixed_len=16
     return out
 
 
-def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1, first_stream=0, cdev=None,
-                    confirm_batch=0):
-    """Full level-1 + level-2 engine on `n_streams` synthetic streams: 10 s
-    prefill, then `n_ticks` ticks launched one at a time (the real-time cadence).
-    With world > 1 every tick also gathers the ranks' positive detections
-    {stream, tick, length, score} to rank 0 over RCCL (easywakeword_amd.shard.gather_positives)."""
+def make_streams(torch, dev, n_streams, seed, word):
+    """The streaming recipe on the GPU: per stream a 16 s loop (160 ticks) of N(0, sigma)
+    noise with five events at jittered positions (half words, half distractors).
+    Returns (period_ticks, pcm[n_streams, period_ticks * 1600] float32)."""
     period_ticks = 160                       # 16 s loop per stream, distinct per stream
     P = period_ticks * 1600
     g = torch.Generator(device=dev)
@@ -301,7 +299,6 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
     pcm = torch.randn((n_streams, P), generator=g, device=dev, dtype=torch.float32) * sig[:, None]
     wl = len(word)
     table = torch.from_numpy(event_sources(word, rng)).to(dev)
-    # five events per 16 s loop per stream at jittered positions: half words, half distractors
     for e in range(5):
         pos = (e * P // 5 + rng.integers(0, 8000, n_streams)).astype(np.int64)
         gain = torch.from_numpy(rng.uniform(0.3, 2.0, n_streams).astype(np.float32)).to(dev)
@@ -310,6 +307,17 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
         idx = torch.from_numpy(pos).to(dev)[:, None] + torch.arange(wl, device=dev)[None, :]
         pcm.scatter_add_(1, idx, src)
     torch.cuda.synchronize()
+    return period_ticks, pcm
+
+
+def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1, first_stream=0, cdev=None,
+                    confirm_batch=0):
+    """Full level-1 + level-2 engine on `n_streams` synthetic streams: 10 s
+    prefill, then `n_ticks` ticks launched one at a time (the real-time cadence).
+    With world > 1 every tick also gathers the ranks' positive detections
+    {stream, tick, length, score} to rank 0 over RCCL (easywakeword_amd.shard.gather_positives)."""
+    period_ticks, pcm = make_streams(torch, dev, n_streams, seed, word)
+    P = period_ticks * 1600
     se = eng_mod.StreamEngine(n_streams, gpu=dev.index if dev.index is not None else 0)
     se.template_from_pcm(word)
     stride = P

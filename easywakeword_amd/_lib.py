@@ -96,6 +96,17 @@ def load():
         if not os.path.exists(LIB_PATH):
             from . import build as _build
             _build.build()
+        # torch bundles its own HIP and HSA runtimes (sonames libamdhip64.so,
+        # libhsa-runtime64.so) beside the system ROCm ones libewk.so links.  When the
+        # system runtime opens the GPU first, torch's runtime later finds no device
+        # (seen on MI355X: "no ROCm-capable device is detected"); the other order works
+        # and device pointers pass between the two.  So torch, when installed, is
+        # imported before libewk.so is opened.
+        if os.environ.get("EWK_NO_TORCH_PRELOAD") != "1":
+            try:
+                import torch  # noqa: F401
+            except Exception:
+                pass
         lib = C.CDLL(LIB_PATH)
         sig = {
             "ewk_default_config": (None, [C.POINTER(EwkConfig)]),

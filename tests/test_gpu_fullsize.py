@@ -1,0 +1,113 @@
+"""Parity at BASELINE.json's full sizes (the bench workloads), checked on samples
+against the oracle and through size-independent properties.
+
+* configs[1]: the bench's 65,536-segment ragged batch (bench.make_segments), scored
+  in one launch: no NaN on audible segments, sampled segments within 1e-4 of the
+  oracle (oracle/mfcc_ref.py, float64 candidates) with identical decisions, and the
+  sampled segments re-scored as their own small batch give bit-identical outputs
+  (a segment's result does not depend on the batch around it or the work order).
+* configs[2]: 8,192 streams of the bench's streaming recipe (bench.make_streams)
+  through the full engine for 70 s of audio (10 s prefill + 60 s): for sampled
+  streams the event list (tick, length, skip flag) equals the oracle gate
+  (oracle/gate_ref.py) exactly, scores within 1e-4, identical decisions.
+"""
+import numpy as np
+import pytest
+
+from golden_io import score_close
+from oracle import mfcc_ref
+from oracle.gate_ref import GateConfig, run_stream
+
+pytestmark = pytest.mark.gpu
+
+SCORE_TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def env():
+    import torch
+    import bench
+    import easywakeword_amd as ewa
+    dev = torch.device("cuda", 0)
+    word = bench.load_word()
+    return torch, bench, ewa, dev, word
+
+
+def test_config2_bench_batch_full_size(env):
+    torch, bench, ewa, dev, word = env
+    n = 65536
+    pcm, off, ln, frames, lengths, offsets = bench.make_segments(torch, dev, n, 1234, word)
+    eng = ewa.Engine()
+    eng.template_from_pcm(word)
+    tm, ts = eng.get_template()
+    mean = torch.empty((n, 20), device=dev)
+    std = torch.empty((n, 20), device=dev)
+    score = torch.empty(n, device=dev, dtype=torch.float64)
+    match = torch.empty(n, device=dev, dtype=torch.uint8)
+    s = torch.cuda.current_stream(dev)
+    eng.score_device(pcm.data_ptr(), off.data_ptr(), ln.data_ptr(), n, mean.data_ptr(), std.data_ptr(),
+                     score.data_ptr(), match.data_ptr(), s.cuda_stream)
+    torch.cuda.synchronize()
+    sc, mt = score.cpu().numpy(), match.cpu().numpy().astype(bool)
+    assert frames == int((1 + lengths.astype(np.int64) // 160).sum())
+    assert not np.isnan(sc).any()                       # every segment is audible
+    assert 0.5 < mt.mean() < 1.0                        # both decisions occur (distractors score ~70)
+
+    rng = np.random.default_rng(5)
+    idx = np.unique(np.concatenate([rng.choice(n, 40, replace=False),
+                                    [int(np.argmax(lengths)), int(np.argmin(lengths)), 0, n - 1]]))
+    segs = [pcm[int(offsets[i]):int(offsets[i]) + int(lengths[i])].cpu().numpy() for i in idx]
+    for i, x in zip(idx, segs):
+        cm, cs = mfcc_ref.extract_mfcc(x.astype(np.float64))
+        ref = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
+        assert score_close(sc[i], ref, SCORE_TOL), (int(i), len(x), sc[i], ref)
+        assert mt[i] == (ref >= 75.0), (int(i), sc[i], ref)
+
+    m2, s2, sc2, mt2 = eng.score(segs, candidate_dtype="float64")
+    np.testing.assert_array_equal(sc2, sc[idx])
+    np.testing.assert_array_equal(m2, mean.cpu().numpy()[idx])
+    np.testing.assert_array_equal(s2, std.cpu().numpy()[idx])
+    np.testing.assert_array_equal(mt2.astype(bool), mt[idx])
+    eng.close()
+
+
+def test_config3_streams_full_size_sampled_vs_oracle(env):
+    torch, bench, ewa, dev, word = env
+    n_streams, ticks = 8192, 700
+    period, pcm = bench.make_streams(torch, dev, n_streams, 1234, word)
+    se = ewa.StreamEngine(n_streams)
+    se.template_from_pcm(word)
+    tm, ts = se.get_template()
+    got = []
+    t = 0
+    while t < ticks:                                   # 32 ticks per call, wrapping at the 16 s loop
+        k = t % period
+        nt = min(32, ticks - t, period - k)
+        se.push_device(pcm.data_ptr() + k * 1600 * 4, period * 1600, 1600, nt)
+        got.append(se.poll())
+        t += nt
+    got.append(se.poll())
+    ev = np.concatenate(got)
+    assert len(ev) > 8 * n_streams                      # ~ 5 events per 16 s per stream after the prefill
+
+    sample = [0, 1, 2, 777, 4095, 4096, 8190, 8191]
+    host = pcm[sample].cpu().numpy()
+    reps = -(-ticks // period)
+    n_checked = 0
+    for row, sid in zip(host, sample):
+        audio = np.tile(row, reps)[: ticks * 1600]
+        ref = run_stream(audio, GateConfig()).events
+        mine = ev[ev["stream"] == sid]
+        mine = mine[np.argsort(mine["tick"], kind="stable")]
+        assert [(int(m["tick"]), int(m["length"]), bool(m["flags"] & 1)) for m in mine] == \
+               [(e.tick, e.length, e.skipped) for e in ref], sid
+        for m, e in zip(mine, ref):
+            if e.skipped:
+                continue
+            cm, cs = mfcc_ref.extract_mfcc(e.audio)
+            s = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
+            assert score_close(float(m["score"]), s, SCORE_TOL), (sid, int(m["tick"]), float(m["score"]), s)
+            assert bool(m["match"]) == (s >= 75.0)
+            n_checked += 1
+    assert n_checked >= 100                             # 138 level-2 calls on these 8 streams
+    se.close()

@@ -202,3 +202,16 @@ def test_confirm_sees_the_normalised_segment():
         assert a.dtype == np.float64 and len(a) == ev["length"]
         assert np.max(np.abs(a)) <= 1.0 and abs(float(np.mean(a))) < 0.05
     assert ww._sound_buffer.engine.state(0)["tick"] == matches[1]["tick"]
+
+
+@pytest.mark.gpu
+def test_torch_usable_after_the_engine_loads():
+    """libewk.so (system ROCm runtime) loaded before torch (its bundled runtime) must
+    leave torch able to use the GPU: _lib.load() imports torch first."""
+    import subprocess
+    import sys
+    code = ("from easywakeword_amd import _lib; assert _lib.device_count() > 0; "
+            "import torch; x = torch.ones(4, device='cuda'); print(float(x.sum()))")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       cwd=os.path.dirname(os.path.dirname(GOLD)))
+    assert r.returncode == 0 and r.stdout.strip().endswith("4.0"), r.stderr[-2000:]
