@@ -43,6 +43,10 @@
 #define EWK_ABLATE 0   // timing-only ablations (scripts/mb_score.py); 0 in every real build
 #endif
 
+#ifndef EWK_ADDTID_STAGE
+#define EWK_ADDTID_STAGE 1   // sample staging with ds_write_addtid_b32 (0: ds_write_b32)
+#endif
+
 #ifndef EWK_TIMING
 #define EWK_TIMING 0   // per-phase s_memtime accounting (scripts/mb_score.py variants only)
 #endif
@@ -63,9 +67,26 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // LDS carve (bytes, every offset a multiple of 16).  The per-lane table rows are
 // transposed to [lane j][index] with a 144-B (36-dword) row pitch so one
 // ds_read_b128 fetches 2 float2 entries and a 16-lane group spans all 64 banks.
+// Frames per wave pass: kNF per 16-lane group (kNF = 2: two independent FFTs per lane).
+constexpr int kFPP = 4 * kNF;
+constexpr int kStageLoads = ((kFPP - 1) * HOP + NFFT + 63) / 64;   // dword loads per lane per pass
+// frame fr's FFT scratch starts at fr * 272 + 8 * (fr >> 2): the two frames a 16-lane
+// group untangles side by side (fr, fr + 4) land 8 banks apart
+constexpr int kScrFrames = kFPP * SCR_FRAME + 8 * (kNF - 1);
+constexpr int kScrFloats = (kScrFrames > 64 * kStageLoads) ? kScrFrames : 64 * kStageLoads;
+// The per-wave FFT scratch (also the sample staging) comes first in LDS: the M0 base of
+// ds_write_addtid_b32 is 16 bits wide, so every wave's scratch must start below 64 KB.
+constexpr int SCR_BYTES = (kScrFloats * 4 + 15) & ~15;
+constexpr int L_SCR = 0;                                  // [wave] kFPP frames x 272 floats
+constexpr int L_TAB = L_SCR + WAVES * SCR_BYTES;
+static_assert(L_SCR + (WAVES - 1) * SCR_BYTES < 65536, "ds_write_addtid_b32 bases must fit M0[15:0]");
+
+// LDS carve (bytes, every offset a multiple of 16).  The per-lane table rows are
+// transposed to [lane j][index] with a 144-B (36-dword) row pitch so one
+// ds_read_b128 fetches 2 float2 entries and a 16-lane group spans all 64 banks.
 constexpr int TP = 18;                                    // float2 pitch of a [j][16] table row
 constexpr int WP = 52;                                    // float pitch of the [j][48] mel weight row (13 chunks: b128/b64 conflict free)
-constexpr int L_WIN2 = 0;                                 // [j][n1] = win2[16*n1 + j]
+constexpr int L_WIN2 = L_TAB;                             // [j][n1] = win2[16*n1 + j]
 constexpr int L_TW1 = L_WIN2 + 16 * TP * 8;               // [j][k1-1] = tw1[16*k1 + j], k1 = 1..15
 constexpr int L_TW2 = L_TW1 + 16 * TP * 8;                // [j][k2] = tw2[j + 16*k2]
 constexpr int L_WPAD = L_TW2 + 16 * TP * 8;               // [j][kMelOff[i] + q] = wpad[16*(it0_i + q) + j]
@@ -77,16 +98,7 @@ constexpr int L_DCT = L_BLO + NMEL * 4;
 constexpr int DCT_ROWS = NMFCC + 1;
 constexpr int DCT_HP = 36;
 constexpr int L_SHARED_END = ((L_DCT + 4 * DCT_ROWS * DCT_HP * 4) + 15) & ~15;
-// Frames per wave pass: kNF per 16-lane group (kNF = 2: two independent FFTs per lane).
-constexpr int kFPP = 4 * kNF;
-constexpr int kStageLoads = ((kFPP - 1) * HOP + NFFT + 63) / 64;   // dword loads per lane per pass
-// frame fr's FFT scratch starts at fr * 272 + 8 * (fr >> 2): the two frames a 16-lane
-// group untangles side by side (fr, fr + 4) land 8 banks apart
-constexpr int kScrFrames = kFPP * SCR_FRAME + 8 * (kNF - 1);
-constexpr int kScrFloats = (kScrFrames > 64 * kStageLoads) ? kScrFrames : 64 * kStageLoads;
-constexpr int W_SCR = 0;                                  // kFPP frames x 272 floats (also the sample staging)
-constexpr int W_TILE = W_SCR + kScrFloats * 4;            // 16 x 128 floats, XOR-swizzled rows
-constexpr int W_MISC = W_SCR;                             // 64 floats, aliases the FFT scratch (epilogue only)
+constexpr int W_TILE = 0;                                 // 16 x 128 floats, XOR-swizzled rows
 constexpr int W_TMIN = W_TILE + 16 * NMEL * 4;            // per-tile log-mel minima (kLmTiles floats)
 constexpr int W_BYTES = W_TMIN + ((kLmTiles * 4 + 15) & ~15);
 constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
@@ -164,6 +176,20 @@ __device__ __forceinline__ constexpr int dperm(int k) { return 4 * (k & 3) + (k 
 // bank-conflict free; the parking copy moves the tile as a flat array.
 __device__ __forceinline__ int tile_swz(int r) { return (r & 14) | ((r & 1) << 4); }
 
+#if EWK_PAIR
+// FFT transpose image of one pass (one real or imaginary plane): row k1 of frame set g
+// holds the 64 lanes' values (16 f + j) contiguously, as ds_write_addtid_b32 stores them
+// (address = M0 + offset + 4 lane).  Rows are placed so that the untangle's row reads
+// -- lane (f, h, j') fetches rows j' and 16 - j' (8 for j' = 0) of frame set h with
+// ds_read_b128 -- hit 16 distinct bank quads in every lane group: the row of (r, h)
+// starts at quad (j'(r) & 3) + 8 h (mod 16), rows sorted by that shift.
+__host__ __device__ constexpr int tr_off(int r, int h) {
+    const int jp = r < 8 ? r : (r == 8 ? 0 : 16 - r);
+    const int q = (jp >> 2) + (r >= 8 ? 2 : 0);
+    return 64 * (16 * h + 4 * (jp & 3) + q) + 4 * ((jp & 3) + 8 * h);   // floats
+}
+#endif
+
 // Segment samples through a buffer descriptor: the hardware range check returns 0
 // outside [0, len) (negative offsets wrap to huge unsigned ones), which is exactly
 // stft(center=True, pad_mode='constant').  Ring segments wrap at the stream ring.
@@ -214,9 +240,40 @@ __device__ __forceinline__ void stage_load(const SegSrc<RING>& v, int q0, int la
     }
 }
 
+#if EWK_PAIR
+// 13 lane-contiguous rows of 64 floats with ds_write_addtid_b32 (M0 = stage base, saved
+// and restored; s_nop 0 for the M0 -> LDS hazard): half the LDS cycles of ds_write_b32
+#define EWK_ST13(o)                                                                                            \
+    asm volatile("s_mov_b32 %[sv], m0\n\ts_mov_b32 m0, %[base]\n\ts_nop 0\n\t"                              \
+                 "ds_write_addtid_b32 %[r0] offset:%[o0]\n\tds_write_addtid_b32 %[r1] offset:%[o1]\n\t"          \
+                 "ds_write_addtid_b32 %[r2] offset:%[o2]\n\tds_write_addtid_b32 %[r3] offset:%[o3]\n\t"          \
+                 "ds_write_addtid_b32 %[r4] offset:%[o4]\n\tds_write_addtid_b32 %[r5] offset:%[o5]\n\t"          \
+                 "ds_write_addtid_b32 %[r6] offset:%[o6]\n\tds_write_addtid_b32 %[r7] offset:%[o7]\n\t"          \
+                 "ds_write_addtid_b32 %[r8] offset:%[o8]\n\tds_write_addtid_b32 %[r9] offset:%[o9]\n\t"          \
+                 "ds_write_addtid_b32 %[r10] offset:%[o10]\n\tds_write_addtid_b32 %[r11] offset:%[o11]\n\t"      \
+                 "ds_write_addtid_b32 %[r12] offset:%[o12]\n\ts_mov_b32 m0, %[sv]"                                 \
+                 : [sv] "=&s"(m0save)                                                                          \
+                 : [base] "s"(m0base), [r0] "v"(r[o]), [r1] "v"(r[o + 1]), [r2] "v"(r[o + 2]), [r3] "v"(r[o + 3]), \
+                   [r4] "v"(r[o + 4]), [r5] "v"(r[o + 5]), [r6] "v"(r[o + 6]), [r7] "v"(r[o + 7]),                \
+                   [r8] "v"(r[o + 8]), [r9] "v"(r[o + 9]), [r10] "v"(r[o + 10]), [r11] "v"(r[o + 11]),          \
+                   [r12] "v"(r[o + 12]), [o0] "i"(256 * (o)), [o1] "i"(256 * (o + 1)), [o2] "i"(256 * (o + 2)), \
+                   [o3] "i"(256 * (o + 3)), [o4] "i"(256 * (o + 4)), [o5] "i"(256 * (o + 5)),                    \
+                   [o6] "i"(256 * (o + 6)), [o7] "i"(256 * (o + 7)), [o8] "i"(256 * (o + 8)),                    \
+                   [o9] "i"(256 * (o + 9)), [o10] "i"(256 * (o + 10)), [o11] "i"(256 * (o + 11)),                \
+                   [o12] "i"(256 * (o + 12))                                                                     \
+                 : "memory")
+static_assert(kStageLoads == 26, "stage_store writes two blocks of 13 rows");
+#endif
 __device__ __forceinline__ void stage_store(float* stage, int lane, const float (&r)[kStageLoads]) {
+#if EWK_PAIR && EWK_ADDTID_STAGE
+    const uint32_t m0base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)stage);
+    uint32_t m0save;
+    EWK_ST13(0);
+    EWK_ST13(13);
+#else
 #pragma unroll
     for (int c = 0; c < kStageLoads; ++c) stage[64 * c + lane] = r[c];
+#endif
 }
 
 constexpr int kMelW[8] = {2, 2, 2, 3, 4, 6, 9, 12};   // per 16-band group (checked on the host)
@@ -351,12 +408,48 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
         for (int k1 = 0; k1 < 16; ++k1) b[g][k1] = a[g][dperm(k1)];
 #else
     {
+#if EWK_PAIR
+        const uint32_t m0base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)scr);
+        const int offA = tr_off(rowA, j >> 3) + 16 * f, offB = tr_off(rowB, j >> 3) + 16 * f;
+#else
         const int jc = 4 * (j >> 2), jl = j & 3;
-#if !EWK_PAIR
         const int rsw = (j >> 2) & 3;
 #endif
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
+#if EWK_PAIR
+#pragma unroll
+            for (int g = 0; g < kNF; ++g) {
+                float w[16];
+#pragma unroll
+                for (int k1 = 0; k1 < 16; ++k1) w[k1] = half ? a[g][dperm(k1)].y : a[g][dperm(k1)].x;
+                // M0 is compiler-reserved: saved and restored in the same statement; the
+                // s_nop covers the M0-write -> LDS-use hazard (without it the stores use the old M0)
+                uint32_t m0save;
+                asm volatile("s_mov_b32 %[sv], m0\n\ts_mov_b32 m0, %[base]\n\ts_nop 0\n\t"
+                             "ds_write_addtid_b32 %[w0] offset:%[o0]\n\tds_write_addtid_b32 %[w1] offset:%[o1]\n\t"
+                             "ds_write_addtid_b32 %[w2] offset:%[o2]\n\tds_write_addtid_b32 %[w3] offset:%[o3]\n\t"
+                             "ds_write_addtid_b32 %[w4] offset:%[o4]\n\tds_write_addtid_b32 %[w5] offset:%[o5]\n\t"
+                             "ds_write_addtid_b32 %[w6] offset:%[o6]\n\tds_write_addtid_b32 %[w7] offset:%[o7]\n\t"
+                             "ds_write_addtid_b32 %[w8] offset:%[o8]\n\tds_write_addtid_b32 %[w9] offset:%[o9]\n\t"
+                             "ds_write_addtid_b32 %[w10] offset:%[o10]\n\tds_write_addtid_b32 %[w11] offset:%[o11]\n\t"
+                             "ds_write_addtid_b32 %[w12] offset:%[o12]\n\tds_write_addtid_b32 %[w13] offset:%[o13]\n\t"
+                             "ds_write_addtid_b32 %[w14] offset:%[o14]\n\tds_write_addtid_b32 %[w15] offset:%[o15]\n\t"
+                             "s_mov_b32 m0, %[sv]"
+                             : [sv] "=&s"(m0save)
+                             : [base] "s"(m0base), [w0] "v"(w[0]), [w1] "v"(w[1]), [w2] "v"(w[2]), [w3] "v"(w[3]),
+                               [w4] "v"(w[4]), [w5] "v"(w[5]), [w6] "v"(w[6]), [w7] "v"(w[7]), [w8] "v"(w[8]),
+                               [w9] "v"(w[9]), [w10] "v"(w[10]), [w11] "v"(w[11]), [w12] "v"(w[12]),
+                               [w13] "v"(w[13]), [w14] "v"(w[14]), [w15] "v"(w[15]),
+                               [o0] "i"(4 * tr_off(0, g)), [o1] "i"(4 * tr_off(1, g)), [o2] "i"(4 * tr_off(2, g)),
+                               [o3] "i"(4 * tr_off(3, g)), [o4] "i"(4 * tr_off(4, g)), [o5] "i"(4 * tr_off(5, g)),
+                               [o6] "i"(4 * tr_off(6, g)), [o7] "i"(4 * tr_off(7, g)), [o8] "i"(4 * tr_off(8, g)),
+                               [o9] "i"(4 * tr_off(9, g)), [o10] "i"(4 * tr_off(10, g)), [o11] "i"(4 * tr_off(11, g)),
+                               [o12] "i"(4 * tr_off(12, g)), [o13] "i"(4 * tr_off(13, g)), [o14] "i"(4 * tr_off(14, g)),
+                               [o15] "i"(4 * tr_off(15, g))
+                             : "memory");
+            }
+#else
 #pragma unroll
             for (int g = 0; g < kNF; ++g)
 #pragma unroll
@@ -364,18 +457,17 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
                     const float2 vv = a[g][dperm(k1)];
                     sc[g][16 * k1 + (jc ^ (4 * ((k1 >> 2) & 3))) + jl] = half ? vv.y : vv.x;
                 }
+#endif
             lds_order();
 #if EWK_PAIR
             // lane (h, j') = (j >> 3, j & 7) reads two columns of frame 4h + f: c0 = j' and its
             // conjugate partner 16 - j' (column 8 beside column 0 for j' = 0)
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) {
-                const int r = s2 ? rowB : rowA;
-                const float4* rd = reinterpret_cast<const float4*>(scf + 16 * r);
-                const int rs = (r >> 2) & 3;
+                const float4* rd = reinterpret_cast<const float4*>(scr + (s2 ? offB : offA));
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
-                    const float4 q = rd[c ^ rs];
+                    const float4 q = rd[c];
                     if (half) {
                         b[s2][4 * c].y = q.x; b[s2][4 * c + 1].y = q.y; b[s2][4 * c + 2].y = q.z; b[s2][4 * c + 3].y = q.w;
                     } else {
@@ -1042,14 +1134,14 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
     if (wave == 0) {
         double mean = 0.0, sd = 0.0;
         if (lane < NMFCC) {
-            const double* p0 = reinterpret_cast<const double*>(smem + L_SHARED_END + W_SCR);
+            const double* p0 = reinterpret_cast<const double*>(smem + L_SCR);
             const double r0 = p0[3 * lane + 2];
             double S1 = 0.0, S2 = 0.0;
             for (int w = 0; w < WAVES; ++w) {
                 int n = 0;   // valid frames of wave w's tiles
                 for (int ti = w; ti < ntile; ti += WAVES) n += min(16, T - 16 * ti);
                 if (n == 0) continue;
-                const double* pw = reinterpret_cast<const double*>(smem + L_SHARED_END + w * W_BYTES + W_SCR);
+                const double* pw = reinterpret_cast<const double*>(smem + L_SCR + w * SCR_BYTES);
                 const double a1 = pw[3 * lane], a2 = pw[3 * lane + 1], d = pw[3 * lane + 2] - r0;
                 S1 += a1 + (double)n * d;
                 S2 += a2 + 2.0 * d * a1 + (double)n * d * d;
@@ -1245,7 +1337,7 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
         count = min(*a.n_events, a.n_seg) - base;
     }
     unsigned char* wbase = smem + L_SHARED_END + wave * W_BYTES;
-    float* scr = reinterpret_cast<float*>(wbase + W_SCR);
+    float* scr = reinterpret_cast<float*>(smem + L_SCR + wave * SCR_BYTES);
     float* tile = reinterpret_cast<float*>(wbase + W_TILE);
     float4* gscr = reinterpret_cast<float4*>(a.lm_scratch) + (int64_t)(blockIdx.x * WAVES + wave) * a.lm_tiles * 10 * 64;
     float* tmins = reinterpret_cast<float*>(wbase + W_TMIN);
@@ -1269,7 +1361,7 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
     const float tsf = (a.has_template && act) ? a.tmpl[NMFCC + lane] : 0.0f;
     if (RING) {   // one segment per workgroup at a time, its tiles spread over the waves
         int* wg_idx = reinterpret_cast<int*>(smem + L_WG);
-        float* misc0 = reinterpret_cast<float*>(smem + L_SHARED_END + W_MISC);
+        float* misc0 = reinterpret_cast<float*>(smem + L_SCR);   // wave 0's FFT scratch (epilogue only)
         for (;;) {
             if (threadIdx.x == 0) wg_idx[0] = atomicAdd(a.work, 1);
             __syncthreads();
