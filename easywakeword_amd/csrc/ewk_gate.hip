@@ -264,6 +264,9 @@ __device__ __forceinline__ double percentile25_sorted(const double* sorted, int 
     return r;
 }
 
+#ifndef EWK_GATE_DMA
+#define EWK_GATE_DMA 1   // float32 tick ingest by LDS-DMA (0: register chunks)
+#endif
 #ifndef EWK_GATE_WPE
 #define EWK_GATE_WPE 2   // min waves per SIMD the register allocator must allow (4 spills: measured slower)
 #endif
@@ -379,7 +382,7 @@ __device__ __forceinline__ double reg_percentile25(const double (&so)[RB], int n
 // whole launch (RB slots per lane, n_blocks <= 64 * RB): loaded once, updated with
 // wave shuffles, stored once -- no dependent global round trips per tick.  RB = 0:
 // both stay in global memory (any n_blocks).
-template <int RB>
+template <int RB, int DMA>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WPE, 8))) void k_gate_ticks(GateArgs g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -411,7 +414,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
 #endif
         }
     };
-    load_chunk(0, 0);
+    // float32 input with the tick staged in LDS: the tick's samples go global -> LDS by
+    // LDS-DMA (global_load_lds), all in flight at once with no VGPRs -- one global round
+    // trip per tick instead of one per register chunk
+    const bool staged = g.stage >= fs && g.stage >= nl;
+    constexpr bool dma = DMA != 0;   // launch_gate: float32 input, tick and window fit the stage
+    auto dma_tick = [&](int t) {
+        const float* src = g.pcm + (int64_t)s * g.stride + (int64_t)t * g.tick_stride;
+        for (int c0 = 0; c0 < fs; c0 += 64) {
+            if (c0 + lane < fs)
+                __builtin_amdgcn_global_load_lds(src + c0 + lane, (__attribute__((address_space(3))) void*)(stage + c0),
+                                                 4, 0, 0);
+        }
+    };
+    if (dma) dma_tick(0);
+    else load_chunk(0, 0);
     GateStream st = g.st[s];
     double* grms = g.block_rms + (int64_t)s * nb;
     double* sorted2 = g.sorted_rms + (int64_t)s * 2 * nb;
@@ -419,7 +436,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
     const PwTree* tbr = trees + kTreeBlockRem;
     const PwTree* tlf = trees + kTreeLastFull;
     const PwTree* tlr = trees + kTreeLastRem;
-    const bool staged = g.stage >= fs && g.stage >= nl;
 #if EWK_GATE_TIMING
     uint64_t gt[8] = {};
 #endif
@@ -453,7 +469,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
         // chunks of kIngestLoads loads per lane in flight before any store (the ring may
         // alias the input as far as the compiler knows: a load-store loop serialises them);
         // chunk 0 of this tick was requested before the previous tick's compute
-        for (int c0 = 0; c0 < fs; c0 += 64 * kIngestLoads) {
+        if (dma) {   // this tick's samples landed in the stage: ring stores from LDS
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wave_sync();
+            for (int c0 = 0; c0 < fs; c0 += 64 * kIngestLoads) {
+#pragma unroll
+                for (int m = 0; m < kIngestLoads; ++m) {
+                    const int i = c0 + lane + 64 * m;
+                    xin[m] = i < fs ? stage[i] : 0.0f;
+                }
+#pragma unroll
+                for (int m = 0; m < kIngestLoads; ++m) {
+                    const int i = c0 + lane + 64 * m;
+                    if (i < fs) {
+                        int k = p0 + i;
+                        if (k >= R) k -= R;
+                        ring[k] = xin[m];
+                    }
+                }
+            }
+        }
+        for (int c0 = 0; c0 < (dma ? 0 : fs); c0 += 64 * kIngestLoads) {
             if (c0 > 0) load_chunk(t, c0);
 #pragma unroll
             for (int m = 0; m < kIngestLoads; ++m) {
@@ -470,7 +506,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
                 }
             }
         }
-        if (t + 1 < g.n_ticks) load_chunk(t + 1, 0);   // next tick's samples, in flight during this tick
+        if (t + 1 < g.n_ticks && !dma) load_chunk(t + 1, 0);   // next tick's samples, in flight during this tick
         __threadfence_block();
         wave_sync();
         const bool wrapped = p0 + fs > R;
@@ -574,6 +610,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
             const double rms = sqrt(sum / (double)nl);
             st.last_rms = rms;
             silent = rms < st.threshold;
+        }
+        if (dma && t + 1 < g.n_ticks) {   // the stage's last reader (a3) has issued its reads
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            dma_tick(t + 1);
         }
         GT_TS(q3);
         GT_ACC(3, q2, q3);
@@ -683,12 +723,17 @@ hipError_t launch_gate(const GateArgs& g, hipStream_t s) {
     const int grid = (g.n_streams + 3) / 4;
     const size_t per_wave = (size_t)g.val_len * 8 + (size_t)g.stage * 4;
     const size_t lds = 4 * per_wave;
-    if (g.n_blocks <= 128)
-        hipLaunchKernelGGL(k_gate_ticks<2>, dim3(grid), dim3(256), lds, s, g);
-    else if (g.n_blocks <= 64 * kGateRegMax)
-        hipLaunchKernelGGL(k_gate_ticks<kGateRegMax>, dim3(grid), dim3(256), lds, s, g);
-    else
-        hipLaunchKernelGGL(k_gate_ticks<0>, dim3(grid), dim3(256), lds, s, g);
+    const int64_t nl = std::min<int64_t>(g.n_last, g.ring_len);
+    const bool dma = EWK_GATE_DMA && g.pcm16 == nullptr && g.stage >= g.block && g.stage >= nl;
+    if (g.n_blocks <= 128) {
+        if (dma) hipLaunchKernelGGL((k_gate_ticks<2, 1>), dim3(grid), dim3(256), lds, s, g);
+        else hipLaunchKernelGGL((k_gate_ticks<2, 0>), dim3(grid), dim3(256), lds, s, g);
+    } else if (g.n_blocks <= 64 * kGateRegMax) {
+        if (dma) hipLaunchKernelGGL((k_gate_ticks<kGateRegMax, 1>), dim3(grid), dim3(256), lds, s, g);
+        else hipLaunchKernelGGL((k_gate_ticks<kGateRegMax, 0>), dim3(grid), dim3(256), lds, s, g);
+    } else {
+        hipLaunchKernelGGL((k_gate_ticks<0, 0>), dim3(grid), dim3(256), lds, s, g);
+    }
     return hipGetLastError();
 }
 
