@@ -147,23 +147,80 @@ __device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2&
     a3 = make_float2(t1.x - t3.y, t1.y + t3.x);   // t1 + i t3
 }
 
+// Second radix-4 stage of the DFT16 with its W16 twiddles folded into FMAs.  Each
+// twiddle is written as a real scale times a (1, tan) factor -- W^1 = C1 (1 - iT),
+// W^3 = C1 (T - i), W^9 = C1 (-1 + iT), W^2 = R2 (1 - i), W^6 = R2 (-1 - i), T = tan(pi/8)
+// -- the two twiddled inputs of a butterfly pair share the scale, and the scale rides
+// in the FMAs of the butterfly outputs: 22 / 20 / 22 instructions for rows k1 = 1 / 2 / 3
+// instead of 28 / 24 / 28 (three complex multiplies + a radix-4 butterfly).
+__device__ __forceinline__ void dft16_stage2(float2 (&x)[16]) {
+    constexpr float C1 = 0.92387953251128674f, R2 = 0.70710678118654752f, T = 0.41421356237309505f;
+    dft4(x[0], x[1], x[2], x[3]);
+    {   // k1 = 1: twiddles W^1, W^2, W^3
+        const float2 a0 = x[4], y1 = x[5], y2 = x[6], y3 = x[7];
+        const float2 u2 = make_float2(y2.x + y2.y, y2.y - y2.x);                        // Y2 (1 - i)
+        const float2 t0 = make_float2(fmaf(R2, u2.x, a0.x), fmaf(R2, u2.y, a0.y));
+        const float2 t1 = make_float2(fmaf(-R2, u2.x, a0.x), fmaf(-R2, u2.y, a0.y));
+        const float2 u1 = make_float2(fmaf(T, y1.y, y1.x), fmaf(-T, y1.x, y1.y));       // Y1 (1 - iT)
+        const float2 u3 = make_float2(fmaf(T, y3.x, y3.y), fmaf(T, y3.y, -y3.x));       // Y3 (T - i)
+        const float2 v2 = make_float2(u1.x + u3.x, u1.y + u3.y), v3 = make_float2(u1.x - u3.x, u1.y - u3.y);
+        x[4] = make_float2(fmaf(C1, v2.x, t0.x), fmaf(C1, v2.y, t0.y));
+        x[6] = make_float2(fmaf(-C1, v2.x, t0.x), fmaf(-C1, v2.y, t0.y));
+        x[5] = make_float2(fmaf(C1, v3.y, t1.x), fmaf(-C1, v3.x, t1.y));                // t1 - i C1 v3
+        x[7] = make_float2(fmaf(-C1, v3.y, t1.x), fmaf(C1, v3.x, t1.y));                // t1 + i C1 v3
+    }
+    {   // k1 = 2: twiddles W^2, W^4 = -i, W^6
+        const float2 a0 = x[8], y1 = x[9], y2 = x[10], y3 = x[11];
+        const float2 t0 = make_float2(a0.x + y2.y, a0.y - y2.x);                        // a0 + (-i Y2)
+        const float2 t1 = make_float2(a0.x - y2.y, a0.y + y2.x);
+        const float2 u1 = make_float2(y1.x + y1.y, y1.y - y1.x);                        // Y1 (1 - i)
+        const float d3 = y3.y - y3.x, n3 = y3.x + y3.y;                                 // Y3 (-1 - i) = (d3, -n3)
+        const float2 v2 = make_float2(u1.x + d3, u1.y - n3), v3 = make_float2(u1.x - d3, u1.y + n3);
+        x[8] = make_float2(fmaf(R2, v2.x, t0.x), fmaf(R2, v2.y, t0.y));
+        x[10] = make_float2(fmaf(-R2, v2.x, t0.x), fmaf(-R2, v2.y, t0.y));
+        x[9] = make_float2(fmaf(R2, v3.y, t1.x), fmaf(-R2, v3.x, t1.y));
+        x[11] = make_float2(fmaf(-R2, v3.y, t1.x), fmaf(R2, v3.x, t1.y));
+    }
+    {   // k1 = 3: twiddles W^3, W^6, W^9
+        const float2 a0 = x[12], y1 = x[13], y2 = x[14], y3 = x[15];
+        const float d2 = y2.y - y2.x, n2 = y2.x + y2.y;                                 // Y2 (-1 - i) = (d2, -n2)
+        const float2 t0 = make_float2(fmaf(R2, d2, a0.x), fmaf(-R2, n2, a0.y));
+        const float2 t1 = make_float2(fmaf(-R2, d2, a0.x), fmaf(R2, n2, a0.y));
+        const float2 u1 = make_float2(fmaf(T, y1.x, y1.y), fmaf(T, y1.y, -y1.x));       // Y1 (T - i)
+        const float m3 = fmaf(T, y3.y, y3.x), u3y = fmaf(T, y3.x, -y3.y);               // Y3 (-1 + iT) = (-m3, u3y)
+        const float2 v2 = make_float2(u1.x - m3, u1.y + u3y), v3 = make_float2(u1.x + m3, u1.y - u3y);
+        x[12] = make_float2(fmaf(C1, v2.x, t0.x), fmaf(C1, v2.y, t0.y));
+        x[14] = make_float2(fmaf(-C1, v2.x, t0.x), fmaf(-C1, v2.y, t0.y));
+        x[13] = make_float2(fmaf(C1, v3.y, t1.x), fmaf(-C1, v3.x, t1.y));
+        x[15] = make_float2(fmaf(-C1, v3.y, t1.x), fmaf(C1, v3.x, t1.y));
+    }
+}
+
 // In-place radix-4x4 DFT16.  On return x[4*k1 + k2] holds X[k1 + 4*k2].
 __device__ __forceinline__ void dft16_perm(float2 (&x)[16]) {
-    constexpr float C1 = 0.92387953251128674f, S1 = 0.38268343236508978f, R2 = 0.70710678118654752f;
 #pragma unroll
     for (int n2 = 0; n2 < 4; ++n2) dft4(x[n2], x[4 + n2], x[8 + n2], x[12 + n2]);
-    // slot 4*k1 + n2 *= W16^(n2*k1)
-    x[4 * 1 + 1] = cmul(x[5], make_float2(C1, -S1));     // W^1
-    x[4 * 1 + 2] = cmul(x[6], make_float2(R2, -R2));     // W^2
-    x[4 * 1 + 3] = cmul(x[7], make_float2(S1, -C1));     // W^3
-    x[4 * 2 + 1] = cmul(x[9], make_float2(R2, -R2));     // W^2
-    x[4 * 2 + 2] = make_float2(x[10].y, -x[10].x);       // W^4 = -i
-    x[4 * 2 + 3] = cmul(x[11], make_float2(-R2, -R2));   // W^6
-    x[4 * 3 + 1] = cmul(x[13], make_float2(S1, -C1));    // W^3
-    x[4 * 3 + 2] = cmul(x[14], make_float2(-R2, -R2));   // W^6
-    x[4 * 3 + 3] = cmul(x[15], make_float2(-C1, S1));    // W^9
+    dft16_stage2(x);
+}
+
+// dft16_perm of the windowed input (x[n].x w[n].x, x[n].y w[n].y): the window products
+// ride in the first stage's FMAs (t0 = fma(x0, w0, x2 w2), t1 = fma(x0, w0, -x2 w2)).
+__device__ __forceinline__ void dft16_perm_win(float2 (&x)[16], const float2 (&w)[16]) {
 #pragma unroll
-    for (int k1 = 0; k1 < 4; ++k1) dft4(x[4 * k1], x[4 * k1 + 1], x[4 * k1 + 2], x[4 * k1 + 3]);
+    for (int n2 = 0; n2 < 4; ++n2) {
+        const float2 x0 = x[n2], x1 = x[4 + n2], x2 = x[8 + n2], x3 = x[12 + n2];
+        const float2 w0 = w[n2], w1 = w[4 + n2], w2 = w[8 + n2], w3 = w[12 + n2];
+        const float2 p2 = make_float2(x2.x * w2.x, x2.y * w2.y), p3 = make_float2(x3.x * w3.x, x3.y * w3.y);
+        const float2 t0 = make_float2(fmaf(x0.x, w0.x, p2.x), fmaf(x0.y, w0.y, p2.y));
+        const float2 t1 = make_float2(fmaf(x0.x, w0.x, -p2.x), fmaf(x0.y, w0.y, -p2.y));
+        const float2 t2 = make_float2(fmaf(x1.x, w1.x, p3.x), fmaf(x1.y, w1.y, p3.y));
+        const float2 t3 = make_float2(fmaf(x1.x, w1.x, -p3.x), fmaf(x1.y, w1.y, -p3.y));
+        x[n2] = make_float2(t0.x + t2.x, t0.y + t2.y);
+        x[8 + n2] = make_float2(t0.x - t2.x, t0.y - t2.y);
+        x[4 + n2] = make_float2(t1.x + t3.y, t1.y - t3.x);   // t1 - i t3
+        x[12 + n2] = make_float2(t1.x - t3.y, t1.y + t3.x);  // t1 + i t3
+    }
+    dft16_stage2(x);
 }
 
 // Natural-order accessor of dft16_perm's output: X[k] lives in slot perm(k).
@@ -317,6 +374,7 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     // (single ds_read_b64s: the compiler would pair them into ds_read2_b64, which
     // costs the LDS twice the cycles per byte)
     float2 a[kNF][16];
+    floatx4 t4[8];   // twiddle row W256^(j*k1)
     {
         float2 x[kNF][16];
 #pragma unroll
@@ -338,30 +396,30 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
                            "+v"(x[g][12]), "+v"(x[g][13]), "+v"(x[g][14]), "+v"(x[g][15])
                          :
                          : "memory");
+        float2 wv[16];
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-            const floatx4 w = w4[c];
+            wv[2 * c] = make_float2(w4[c].x, w4[c].y);
+            wv[2 * c + 1] = make_float2(w4[c].z, w4[c].w);
+        }
+        EWK_TS(p1);
+        if (tim) EWK_TACC(8, p0, p1);
+        // ---- DFT16 over n1 (window folded into its first stage), twiddle W256^(j*k1)
+        // (one twiddle row serves every frame of the lane, requested before the DFT16s)
+        EWK_LD128_8(t4, (uint32_t)(uintptr_t)(reinterpret_cast<const float4*>(smem + L_TW1) + j * (TP / 2)));
 #pragma unroll
-            for (int g = 0; g < kNF; ++g) {
-                a[g][2 * c] = make_float2(x[g][2 * c].x * w.x, x[g][2 * c].y * w.y);
-                a[g][2 * c + 1] = make_float2(x[g][2 * c + 1].x * w.z, x[g][2 * c + 1].y * w.w);
-            }
+        for (int g = 0; g < kNF; ++g) {
+#pragma unroll
+            for (int n = 0; n < 16; ++n) a[g][n] = x[g][n];
+            dft16_perm_win(a[g], wv);
         }
     }
     lds_order();
-    EWK_TS(p1);
-    if (tim) EWK_TACC(8, p0, p1);
     // next pass's samples: issued before the mel stage (registers are free there),
     // stored to the staging area at the end of the pass
     float pf[kStageLoads];
     EWK_TS(p2);
-    if (tim) EWK_TACC(9, p1, p2);
-    // ---- DFT16 over n1, twiddle W256^(j*k1) (one twiddle row serves every frame of the lane)
     {
-        floatx4 t4[8];   // twiddle row, requested before the DFT16s it waits behind
-        EWK_LD128_8(t4, (uint32_t)(uintptr_t)(reinterpret_cast<const float4*>(smem + L_TW1) + j * (TP / 2)));
-#pragma unroll
-        for (int g = 0; g < kNF; ++g) dft16_perm(a[g]);
         EWK_WAIT_8(t4);
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
