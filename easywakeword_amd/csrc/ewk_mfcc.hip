@@ -92,13 +92,18 @@ constexpr int L_TW2 = L_TW1 + 16 * TP * 8;                // [j][k2] = tw2[j + 1
 constexpr int L_WPAD = L_TW2 + 16 * TP * 8;               // [j][kMelOff[i] + q] = wpad[16*(it0_i + q) + j]
 constexpr int L_BLO = L_WPAD + 16 * WP * 4;
 constexpr int L_DCT = L_BLO + NMEL * 4;
-// DCT image for the MFMA A operand, k-major per lane: [h][row][s] = D[row][4s + h] with
-// 36-float runs (two b128 reads fetch a lane's 8 k-steps, at most 2-way bank
-// conflicts); row NMFCC is zero (the acc1 lanes past coefficient 19 read it).
-constexpr int DCT_ROWS = NMFCC + 1;
-constexpr int DCT_HP = 36;
-constexpr int L_SHARED_END = ((L_DCT + 4 * DCT_ROWS * DCT_HP * 4) + 15) & ~15;
-constexpr int W_TILE = 0;                                 // 16 x 128 floats, XOR-swizzled rows
+// DCT operand image for v_mfma_f32_16x16x32_f16: D * 2^10 split into f16 hi + lo (the
+// products hi*hi + hi*lo + lo*hi carry ~22 bits).  The tile's k order groups each lane's
+// eight bands: k-chunk c (k = 8c .. 8c+7) holds bands c + 16 jj, jj = 0..7, so the
+// operand of k-step q for lane l is chunk 4q + (l >> 4).  Row tile 0 (coefficients 0..15):
+// [q][hi/lo][lane] 16-B chunks; row tile 1 (coefficients 16..19): [q][hi/lo][l >> 4][l & 3]
+// for the lanes with (l & 15) < 4, every other lane reads the block's zero chunk.
+constexpr float kDctScale = 1024.0f;
+constexpr int DCT_RT1 = 4 * 2 * 64 * 16;                  // row tile 1: [q][hi/lo] blocks of 17 chunks
+constexpr int DCT_RT1_STRIDE = 17 * 16;                   // 16 data chunks [l >> 4][l & 3] + a zero chunk
+constexpr int DCT_BYTES = DCT_RT1 + 8 * DCT_RT1_STRIDE;
+constexpr int L_SHARED_END = ((L_DCT + DCT_BYTES) + 15) & ~15;
+constexpr int W_TILE = 0;                                 // 16 frame rows x 512 B of f16 hi/lo chunks (tile_chunk)
 constexpr int W_TMIN = W_TILE + 16 * NMEL * 4;            // per-tile log-mel minima (kLmTiles floats)
 constexpr int W_BYTES = W_TMIN + ((kLmTiles * 4 + 15) & ~15);
 constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
@@ -226,12 +231,65 @@ __device__ __forceinline__ void dft16_perm_win(float2 (&x)[16], const float2 (&w
 // Natural-order accessor of dft16_perm's output: X[k] lives in slot perm(k).
 __device__ __forceinline__ constexpr int dperm(int k) { return 4 * (k & 3) + (k >> 2); }
 
-// Log-mel tile: 16 frame rows x 128 bands, row r holds band m at column m ^ swz(r).
-// swz(r) takes 16 distinct even values for r = 0..15 and flips bit 4 between rows
-// 2p and 2p+1, so the mel stage's row-pair writes (ds_write_b32, 32-bank halves)
-// and the MFMA B-operand reads (16 rows x 2 k-lanes per half) are both
-// bank-conflict free; the parking copy moves the tile as a flat array.
-__device__ __forceinline__ int tile_swz(int r) { return (r & 14) | ((r & 1) << 4); }
+
+// f16 hi/lo split of a float32: hi = x truncated to f16's 11 significant bits (exact in
+// f16 over the dB range), lo = x - hi exactly, stored to f16 with round-to-nearest, so
+// float(hi) + float(lo) = x within 2^-22 |x|.
+__device__ __forceinline__ float f16_trunc(float x) { return __uint_as_float(__float_as_uint(x) & 0xFFFFE000u); }
+typedef _Float16 halfx2 __attribute__((ext_vector_type(2)));
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ uint32_t pk_f16(float a, float b) {   // v_cvt_pk_f16_f32
+    halfx2 h;
+    h.x = (_Float16)a;
+    h.y = (_Float16)b;
+    return __builtin_bit_cast(uint32_t, h);
+}
+__device__ __forceinline__ float f16_lo(uint32_t p) { return (float)__builtin_bit_cast(halfx2, p).x; }
+__device__ __forceinline__ float f16_hi(uint32_t p) { return (float)__builtin_bit_cast(halfx2, p).y; }
+// eight log-mel values -> their hi chunk and lo chunk (16 B each)
+__device__ __forceinline__ void split8(const float (&x)[8], uint4& hi, uint4& lo) {
+    float h[8], l[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { h[i] = f16_trunc(x[i]); l[i] = x[i] - h[i]; }
+    hi = make_uint4(pk_f16(h[0], h[1]), pk_f16(h[2], h[3]), pk_f16(h[4], h[5]), pk_f16(h[6], h[7]));
+    lo = make_uint4(pk_f16(l[0], l[1]), pk_f16(l[2], l[3]), pk_f16(l[4], l[5]), pk_f16(l[6], l[7]));
+}
+// Byte offset of k-chunk c of frame row r in the log-mel tile: the row's hi chunks fill its
+// first 256 B and the lo chunks the next 256 B, chunk c at slot c ^ r, so the 16 rows of a
+// DCT operand read (one chunk per row) and the 16 chunks of a row write both cover all
+// 64 banks.
+__device__ __forceinline__ int tile_chunk(int r, int c) { return 512 * r + 16 * (c ^ r); }
+
+// top_db clamp of a parked tile (its flat 8 KB image `src`): lane l takes the chunk pairs
+// p = l + 64 u (frame row p >> 4, slot p & 15), rebuilds each value exactly as
+// float(hi) + float(lo), clamps it at theta and writes the re-split pair back in place.
+__device__ __forceinline__ void clamp_load(const float4* src, int lane, uint4 (&h)[4], uint4 (&l)[4]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int p = lane + 64 * u;
+        h[u] = __builtin_bit_cast(uint4, src[32 * (p >> 4) + (p & 15)]);
+        l[u] = __builtin_bit_cast(uint4, src[32 * (p >> 4) + 16 + (p & 15)]);
+    }
+}
+__device__ __forceinline__ void clamp_store(float* tile, int lane, const uint4 (&h)[4], const uint4 (&l)[4],
+                                            float theta) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t hw[4] = {h[u].x, h[u].y, h[u].z, h[u].w}, lw[4] = {l[u].x, l[u].y, l[u].z, l[u].w};
+        float x[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            x[2 * k] = fmaxf(f16_lo(hw[k]) + f16_lo(lw[k]), theta);
+            x[2 * k + 1] = fmaxf(f16_hi(hw[k]) + f16_hi(lw[k]), theta);
+        }
+        uint4 hh, ll;
+        split8(x, hh, ll);
+        const int p = lane + 64 * u;
+        uint4* dst = reinterpret_cast<uint4*>(tile) + 32 * (p >> 4) + (p & 15);
+        dst[0] = hh;
+        dst[16] = ll;
+    }
+}
 
 #if EWK_PAIR
 // FFT transpose image of one pass (one real or imaginary plane): row k1 of frame set g
@@ -350,7 +408,7 @@ template <int RING>
 __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T, int row0, bool next,
                                            const unsigned char* smem, float* scr, float* tile,
                                            int lane, const int (&lo)[8], float& vmax, float& vmin,
-                                           uint64_t* tim = nullptr) {
+                                           float clampv = -INFINITY, uint64_t* tim = nullptr) {
     EWK_TS(p0);
     // lane group f = lane>>4 holds frames fr = 4 g + f (g < kNF) of this pass; the
     // kNF frames of a lane are independent instruction streams (ILP for the wave).
@@ -707,25 +765,27 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     EWK_TS(p7);
     if (tim) EWK_TACC(14, p6, p7);
     lds_order();
+    // Rows of frames past T keep their (finite: silence gives -100 dB) values: the DCT
+    // columns are independent and the statistics skip those frames, so only the frame's
+    // max/min needs the validity test, once per frame.  The eight bands of a lane form
+    // k-chunk j of its frame row (hi and lo halves, one ds_write_b128 each).
 #pragma unroll
     for (int g = 0; g < kNF; ++g) {
         const int r = row0 + 4 * g + f;
-        const int sw = tile_swz(r);
-        const int jx = j ^ (sw & 15), sb = sw >> 4;
-        float* re = tile + r * NMEL + jx + 16 * sb;   // even i: column 16*(i+sb) + jx
-        float* ro = tile + r * NMEL + jx - 16 * sb;   // odd  i: column 16*(i-sb) + jx
-        // Rows of frames past T keep their (finite: silence gives -100 dB) values: the
-        // DCT columns are independent and the statistics skip those frames, so only
-        // the frame's max/min needs the validity test, once per frame.
-        float fmx = db[g][0], fmn = db[g][0];
+        float fmx = db[g][0], fmn = db[g][0], x[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             fmx = fmaxf(fmx, db[g][i]);
             fmn = fminf(fmn, db[g][i]);
-            ((i & 1) ? ro : re)[16 * i] = db[g][i];
+            x[i] = fmaxf(db[g][i], clampv);   // top_db recompute path; -inf folds away otherwise
         }
         vmax = fmaxf(vmax, valid[g] ? fmx : -INFINITY);
         vmin = fminf(vmin, valid[g] ? fmn : INFINITY);
+        uint4 hi, lo;
+        split8(x, hi, lo);
+        unsigned char* tb = reinterpret_cast<unsigned char*>(tile) + tile_chunk(r, j);
+        *reinterpret_cast<uint4*>(tb) = hi;
+        *reinterpret_cast<uint4*>(tb + 256) = lo;
     }
     lds_order();
     EWK_TS(p8);
@@ -736,66 +796,73 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     if (tim) EWK_TACC(16, p8, p9);
 }
 
-// DCT of one 16-frame log-mel tile on the matrix cores.
-// Lane l gets C[row = 4h + r][frame col] of both row tiles (h = l>>4, col = l&15) in c[0..3], c[4..7].
-// The operands of 8 k-steps (2+2 b128 of the DCT image, 8 tile reads) are requested one
-// block ahead of the 16 MFMAs that consume them (counted lgkmcnt, 12 reads per block).
-#define EWK_DCT_LOAD(p, blk)                                                                         \
-    do {                                                                                             \
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(A0[p][0]) : "v"(a0), "i"(32 * (blk)) : "memory");      \
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(A0[p][1]) : "v"(a0), "i"(32 * (blk) + 16) : "memory"); \
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(A1[p][0]) : "v"(a1), "i"(32 * (blk)) : "memory");      \
-        asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(A1[p][1]) : "v"(a1), "i"(32 * (blk) + 16) : "memory"); \
-        EWK_DCT_LB(p, blk, 0); EWK_DCT_LB(p, blk, 1); EWK_DCT_LB(p, blk, 2); EWK_DCT_LB(p, blk, 3);                 \
-        EWK_DCT_LB(p, blk, 4); EWK_DCT_LB(p, blk, 5); EWK_DCT_LB(p, blk, 6); EWK_DCT_LB(p, blk, 7);                 \
+// DCT of one 16-frame log-mel tile on the matrix cores: C[32 x 16] = D[32 x 128] X[128 x 16]
+// with v_mfma_f32_16x16x32_f16 on the f16 hi/lo splits, three products per k-step
+// (Dh Xh + Dh Xl + Dl Xh, f32 accumulation; the dropped Dl Xl is ~2^-22 relative).
+// Lane l gets C[row = 4h + r][frame col] of both row tiles (h = l>>4, col = l&15) in
+// c[0..3], c[4..7] -- the layout of the f32 16x16x4 MFMA.  The operands of k-step q
+// (6 ds_read_b128) are requested one step ahead of its 6 MFMAs.
+#define EWK_DCT_RD(dst, addr, off) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(off) : "memory")
+#define EWK_DCT_LOAD(p, q)                                                   \
+    do {                                                                     \
+        EWK_DCT_RD(Bh[p], bq[q], 0);                                         \
+        EWK_DCT_RD(Bl[p], bq[q], 256);                                       \
+        EWK_DCT_RD(A0h[p], a0, 2048 * (q));                                  \
+        EWK_DCT_RD(A0l[p], a0, 2048 * (q) + 1024);                           \
+        EWK_DCT_RD(A1h[p], a1, DCT_RT1_STRIDE * (2 * (q)));                  \
+        EWK_DCT_RD(A1l[p], a1, DCT_RT1_STRIDE * (2 * (q) + 1));              \
     } while (0)
-#define EWK_DCT_LB(p, blk, u) \
-    asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(B[p][u]) : "v"(bb[u]), "i"(128 * (blk)) : "memory")
-#define EWK_DCT_WAIT(p, n)                                                                                     \
-    asm volatile("s_waitcnt lgkmcnt(" #n ")"                                                                   \
-                 : "+v"(A0[p][0]), "+v"(A0[p][1]), "+v"(A1[p][0]), "+v"(A1[p][1]), "+v"(B[p][0]), "+v"(B[p][1]), \
-                   "+v"(B[p][2]), "+v"(B[p][3]), "+v"(B[p][4]), "+v"(B[p][5]), "+v"(B[p][6]), "+v"(B[p][7])      \
-                 :                                                                                             \
+#define EWK_DCT_WAIT(p, n)                                                                               \
+    asm volatile("s_waitcnt lgkmcnt(" #n ")"                                                             \
+                 : "+v"(Bh[p]), "+v"(Bl[p]), "+v"(A0h[p]), "+v"(A0l[p]), "+v"(A1h[p]), "+v"(A1l[p]) \
+                 :                                                                                       \
                  : "memory")
+#define EWK_MF(a, b, acc) \
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8, a), __builtin_bit_cast(halfx8, b), acc, 0, 0, 0)
+#if EWK_ABLATE & 256   // timing probe: the DCT operands are read but only one MFMA per k-step runs
+#define EWK_DCT_MFMA(p) EWK_MF(A0h[p] + A1l[p], Bh[p] + Bl[p], acc0);
+#else
 #define EWK_DCT_MFMA(p)                                                                        \
-    _Pragma("unroll") for (int u = 0; u < 8; ++u) {                                            \
-        acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(A0[p][u >> 2][u & 3], B[p][u], acc0, 0, 0, 0); \
-        acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(A1[p][u >> 2][u & 3], B[p][u], acc1, 0, 0, 0); \
-    }
+    do {                                                                                       \
+        EWK_MF(A0h[p], Bh[p], acc0); EWK_MF(A1h[p], Bh[p], acc1);                              \
+        EWK_MF(A0h[p], Bl[p], acc0); EWK_MF(A1h[p], Bl[p], acc1);                              \
+        EWK_MF(A0l[p], Bh[p], acc0); EWK_MF(A1l[p], Bh[p], acc1);                              \
+    } while (0)
+#endif
 __device__ __forceinline__ void tile_dct(const float* tile, const float* s_dct, int lane, float (&c)[8]) {
-    const int col = lane & 15, h = lane >> 4;
+    const int col = lane & 15, g4 = lane >> 4;
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-    // B[k = 4s + h][col] = tile row col, band 4s + h, stored at column (4s + h) ^ swz(col);
-    // swz < 32, so bands 32u + b sit at 32u + (b ^ swz): 8 per-lane addresses + immediates.
-    const int sw = tile_swz(col);
-    const uint32_t tb = (uint32_t)(uintptr_t)tile;
-    uint32_t bb[8];
+    // B of k-step q: chunk 4q + g4 of frame row col, at slot (4q + g4) ^ col =
+    // 4 (q ^ (col >> 2)) + (g4 ^ (col & 3))
+    const uint32_t tb = (uint32_t)(uintptr_t)tile + 512 * col + 16 * (g4 ^ (col & 3));
+    uint32_t bq[4];
 #pragma unroll
-    for (int s = 0; s < 8; ++s) bb[s] = tb + 4 * (col * NMEL + ((4 * s + h) ^ sw));
-    const uint32_t a0 = (uint32_t)(uintptr_t)(s_dct + (h * DCT_ROWS + col) * DCT_HP);
-    const uint32_t a1 = (uint32_t)(uintptr_t)(s_dct + (h * DCT_ROWS + (col < 4 ? 16 + col : NMFCC)) * DCT_HP);
-    floatx4 A0[2][2], A1[2][2];
-    float B[2][8];
+    for (int q = 0; q < 4; ++q) bq[q] = tb + 64 * (q ^ (col >> 2));
+    const uint32_t db = (uint32_t)(uintptr_t)s_dct;
+    const uint32_t a0 = db + 16 * lane;
+    const uint32_t a1 = db + DCT_RT1 + 16 * (col < 4 ? 4 * g4 + col : 16);
+    floatx4 Bh[2], Bl[2], A0h[2], A0l[2], A1h[2], A1l[2];
     EWK_DCT_LOAD(0, 0);
     EWK_DCT_LOAD(1, 1);
-    EWK_DCT_WAIT(0, 12);
+    EWK_DCT_WAIT(0, 6);
     EWK_DCT_MFMA(0);
     EWK_DCT_LOAD(0, 2);
-    EWK_DCT_WAIT(1, 12);
+    EWK_DCT_WAIT(1, 6);
     EWK_DCT_MFMA(1);
     EWK_DCT_LOAD(1, 3);
-    EWK_DCT_WAIT(0, 12);
+    EWK_DCT_WAIT(0, 6);
     EWK_DCT_MFMA(0);
     EWK_DCT_WAIT(1, 0);
     EWK_DCT_MFMA(1);
     lds_order();
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { c[i] = acc0[i]; c[4 + i] = acc1[i]; }
+    for (int i = 0; i < 4; ++i) { c[i] = acc0[i] * (1.0f / kDctScale); c[4 + i] = acc1[i] * (1.0f / kDctScale); }
 }
+#undef EWK_DCT_RD
 #undef EWK_DCT_LOAD
-#undef EWK_DCT_LB
 #undef EWK_DCT_WAIT
 #undef EWK_DCT_MFMA
+#undef EWK_MF
 
 // fp64 shifted sums of the frame columns that exist (d = c - cref).
 __device__ __forceinline__ void stats_add(const float (&c)[8], const float (&cref)[8], bool ok, double (&s1)[8],
@@ -939,7 +1006,8 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         for (int p = 0; p < 16 / kFPP; ++p) {
             const int pass = tile_i * (16 / kFPP) + p;
             if (pass < npass)
-                frame_pass(v, pass * kFPP, T, p * kFPP, pass + 1 < npass, smem, scr, tile, lane, lo, vmax, tmin, tim);
+                frame_pass(v, pass * kFPP, T, p * kFPP, pass + 1 < npass, smem, scr, tile, lane, lo, vmax, tmin,
+                           -INFINITY, tim);
             else   // rows of frames past T: zero (ignored by the statistics)
                 zero_rows(tile, p * kFPP, lane);
         }
@@ -985,25 +1053,21 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
             // their pass-1 contribution for the clamped one (parked log-mel + DCT columns)
             int cur = 0;
             while (cur < ntile && !(tmins[cur] < theta)) ++cur;
-            float4 nx[8], no0, no1;
+            uint4 nh[4], nl[4];
+            float4 no0, no1;
             if (cur < ntile) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) nx[k] = gscr[(int64_t)cur * 512 + k * 64 + lane];
+                clamp_load(gscr + (int64_t)cur * 512, lane, nh, nl);
                 no0 = gcol[(int64_t)cur * 128 + lane];
                 no1 = gcol[(int64_t)cur * 128 + 64 + lane];
             }
             while (cur < ntile) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    tile4[k * 64 + lane] = make_float4(fmaxf(nx[k].x, theta), fmaxf(nx[k].y, theta),
-                                                       fmaxf(nx[k].z, theta), fmaxf(nx[k].w, theta));
+                clamp_store(tile, lane, nh, nl, theta);
                 const float co[8] = {no0.x, no0.y, no0.z, no0.w, no1.x, no1.y, no1.z, no1.w};
                 lds_order();
                 int nxt = cur + 1;
                 while (nxt < ntile && !(tmins[nxt] < theta)) ++nxt;
                 if (nxt < ntile) {   // next clamped tile's loads overlap this tile's MFMAs
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) nx[k] = gscr[(int64_t)nxt * 512 + k * 64 + lane];
+                    clamp_load(gscr + (int64_t)nxt * 512, lane, nh, nl);
                     no0 = gcol[(int64_t)nxt * 128 + lane];
                     no1 = gcol[(int64_t)nxt * 128 + 64 + lane];
                 }
@@ -1028,16 +1092,10 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
                 for (int p = 0; p < 16 / kFPP; ++p) {
                     const int pass = tile_i * (16 / kFPP) + p;
                     if (pass < npass)
-                        frame_pass(v, pass * kFPP, T, p * kFPP, pass + 1 < npass, smem, scr, tile, lane, lo, d0, d1);
+                        frame_pass(v, pass * kFPP, T, p * kFPP, pass + 1 < npass, smem, scr, tile, lane, lo, d0, d1,
+                                   theta);
                     else
                         zero_rows(tile, p * kFPP, lane);
-                }
-                lds_order();
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const float4 x = tile4[k * 64 + lane];
-                    tile4[k * 64 + lane] = make_float4(fmaxf(x.x, theta), fmaxf(x.y, theta),
-                                                       fmaxf(x.z, theta), fmaxf(x.w, theta));
                 }
                 lds_order();
                 float c[8];
@@ -1080,7 +1138,7 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
     float vmax = -INFINITY, vmin = INFINITY;
-    auto run_tile = [&](int tile_i, float& mx, float& mn) {
+    auto run_tile = [&](int tile_i, float& mx, float& mn, float clampv) {
         {   // stage the tile's first pass
             float r[kStageLoads];
             stage_load(v, tile_i * 16 * HOP - NFFT / 2, lane, r);
@@ -1092,7 +1150,7 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
             const int pass = tile_i * (16 / kFPP) + p;
             if (pass < npass)
                 frame_pass(v, pass * kFPP, T, p * kFPP, p + 1 < 16 / kFPP && pass + 1 < npass, smem, scr, tile, lane,
-                           lo, mx, mn);
+                           lo, mx, mn, clampv);
             else
                 zero_rows(tile, p * kFPP, lane);
         }
@@ -1101,7 +1159,7 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
     for (int lt = 0; lt < nloc; ++lt) {
         const int tile_i = wave + WAVES * lt;
         float tmin = INFINITY;
-        run_tile(tile_i, vmax, tmin);
+        run_tile(tile_i, vmax, tmin, -INFINITY);
         if (park) {
             float4* dst = gscr + (int64_t)lt * 8 * 64 + lane;
             floatx4 t[8];
@@ -1139,11 +1197,10 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
             for (int lt = 0; lt < nloc; ++lt) {
                 if (!(tmins[lt] < theta)) continue;
                 const int tile_i = wave + WAVES * lt;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const float4 x = gscr[(int64_t)lt * 512 + k * 64 + lane];
-                    tile4[k * 64 + lane] = make_float4(fmaxf(x.x, theta), fmaxf(x.y, theta), fmaxf(x.z, theta),
-                                                       fmaxf(x.w, theta));
+                {
+                    uint4 nh[4], nl[4];
+                    clamp_load(gscr + (int64_t)lt * 512, lane, nh, nl);
+                    clamp_store(tile, lane, nh, nl, theta);
                 }
                 const float4 o0 = gcol[(int64_t)lt * 128 + lane], o1 = gcol[(int64_t)lt * 128 + 64 + lane];
                 const float co[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
@@ -1158,14 +1215,7 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
             for (int lt = 0; lt < nloc; ++lt) {
                 const int tile_i = wave + WAVES * lt;
                 float d0 = 0.f, d1 = 0.f;
-                run_tile(tile_i, d0, d1);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const float4 x = tile4[k * 64 + lane];
-                    tile4[k * 64 + lane] = make_float4(fmaxf(x.x, theta), fmaxf(x.y, theta), fmaxf(x.z, theta),
-                                                       fmaxf(x.w, theta));
-                }
-                lds_order();
+                run_tile(tile_i, d0, d1, theta);
                 float c[8];
                 tile_dct(tile, s_dct, lane, c);
                 stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
@@ -1381,10 +1431,31 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
                 if (o >= kMelOff[g] && o < kMelOff[g] + kMelW[g]) w = tab->wpad[(kMelIt0[g] + o - kMelOff[g]) * 16 + j];
             sw[i] = w;
         }
-        float* sd = reinterpret_cast<float*>(smem + L_DCT);
-        for (int i = threadIdx.x; i < 4 * DCT_ROWS * DCT_HP; i += blockDim.x) {
-            const int h = i / (DCT_ROWS * DCT_HP), row = (i / DCT_HP) % DCT_ROWS, k = i % DCT_HP;
-            sd[i] = (row < NMFCC && k < NMEL / 4) ? tab->dct[row * NMEL + 4 * k + h] : 0.0f;
+        // the f16 hi/lo DCT operand chunks (kDctScale keeps the lo parts normal)
+        uint4* sd = reinterpret_cast<uint4*>(smem + L_DCT);
+        for (int i = threadIdx.x; i < DCT_BYTES / 16; i += blockDim.x) {
+            int row = -1, c = 0, hl = 0;
+            if (i < DCT_RT1 / 16) {
+                const int l = i & 63;
+                hl = (i >> 6) & 1;
+                row = l & 15;
+                c = 4 * (i >> 7) + (l >> 4);
+            } else {
+                const int k = i - DCT_RT1 / 16, blk = k / 17, slot = k % 17;   // blk = q * 2 + hl
+                if (slot < 16) {
+                    row = 16 + (slot & 3);
+                    c = 4 * (blk >> 1) + (slot >> 2);
+                    hl = blk & 1;
+                }
+            }
+            float v[8];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const float d = row >= 0 ? tab->dct[row * NMEL + c + 16 * jj] * kDctScale : 0.0f;
+                const float h = f16_trunc(d);
+                v[jj] = hl ? d - h : h;
+            }
+            sd[i] = make_uint4(pk_f16(v[0], v[1]), pk_f16(v[2], v[3]), pk_f16(v[4], v[5]), pk_f16(v[6], v[7]));
         }
     }
     __syncthreads();
