@@ -1001,13 +1001,18 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     float4* tile4 = reinterpret_cast<float4*>(tile);
     for (int tile_i = 0; tile_i < ntile; ++tile_i) {
         float tmin = INFINITY;
+        // speculative top_db clamp at the running max: the final threshold can only be
+        // higher, and max(max(x, run), final) = max(x, final), so a tile stored clamped at
+        // `run` is exact when the segment max is already known and is fixed up from its
+        // parked (partly clamped) copy otherwise
+        const float run = park ? wave_max(vmax) - 80.0f : -INFINITY;
         EWK_TS(t0);
 #pragma unroll 1
         for (int p = 0; p < 16 / kFPP; ++p) {
             const int pass = tile_i * (16 / kFPP) + p;
             if (pass < npass)
                 frame_pass(v, pass * kFPP, T, p * kFPP, pass + 1 < npass, smem, scr, tile, lane, lo, vmax, tmin,
-                           -INFINITY, tim);
+                           run, tim);
             else   // rows of frames past T: zero (ignored by the statistics)
                 zero_rows(tile, p * kFPP, lane);
         }
@@ -1035,7 +1040,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
             dst[64] = make_float4(c[4], c[5], c[6], c[7]);
         }
         vmin = fminf(vmin, tmin);
-        tmin = wave_min(tmin);
+        tmin = fmaxf(wave_min(tmin), run);   // the stored tile's minimum
         if (lane == 0) tmins[min(tile_i, kLmTiles - 1)] = tmin;   // kLmTiles slots: only the parked path reads them
         EWK_TS(t2);
         EWK_TACC(1, t1, t2);
@@ -1159,7 +1164,8 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
     for (int lt = 0; lt < nloc; ++lt) {
         const int tile_i = wave + WAVES * lt;
         float tmin = INFINITY;
-        run_tile(tile_i, vmax, tmin, -INFINITY);
+        const float run = park ? wave_max(vmax) - 80.0f : -INFINITY;   // speculative clamp (segment_stats)
+        run_tile(tile_i, vmax, tmin, run);
         if (park) {
             float4* dst = gscr + (int64_t)lt * 8 * 64 + lane;
             floatx4 t[8];
@@ -1181,7 +1187,7 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
             dst[64] = make_float4(c[4], c[5], c[6], c[7]);
         }
         vmin = fminf(vmin, tmin);
-        tmin = wave_min(tmin);
+        tmin = fmaxf(wave_min(tmin), run);
         if (lane == 0) tmins[min(lt, kLmTiles - 1)] = tmin;
     }
     vmax = wave_max(vmax);
