@@ -39,6 +39,9 @@
 #ifndef EWK_GATE_NT
 #define EWK_GATE_NT 1   // 1: non-temporal tick loads (read once; measured -6%), 2: also non-temporal ring stores (no gain)
 #endif
+#ifndef EWK_GATE_ABLATE
+#define EWK_GATE_ABLATE 0   // timing-only ablations (scripts/mb_gate.py): 1 no a2, 2 no ring stores, 4 no tick loads
+#endif
 #ifndef EWK_GATE_TIMING
 #define EWK_GATE_TIMING 0   // per-phase s_memtime accounting (scripts/mb_gate.py variants only)
 #endif
@@ -265,11 +268,12 @@ __device__ __forceinline__ double percentile25_sorted(const double* sorted, int 
 }
 
 #ifndef EWK_GATE_DMA
-#define EWK_GATE_DMA 1   // float32 tick ingest by LDS-DMA (0: register chunks)
+#define EWK_GATE_DMA 2   // float32 tick ingest by LDS-DMA (0: register chunks, 1: 4-B pieces, 2: 16-B pieces when aligned)
 #endif
 #ifndef EWK_GATE_WPE
 #define EWK_GATE_WPE 2   // min waves per SIMD the register allocator must allow (4 spills: measured slower)
 #endif
+constexpr int kDma4Chunks = 8;     // 16-B DMA path: ticks of up to 8 * 256 samples copied to the ring in one batch
 constexpr int kIngestLoads = 4;    // tick samples per lane loaded ahead of the ring stores (16: 166 VGPRs, 3 waves/SIMD, 10 % slower)
 
 // ---- register-resident block RMS multiset (n_blocks <= 64 * RB) ------------------
@@ -421,6 +425,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
     constexpr bool dma = DMA != 0;   // launch_gate: float32 input, tick and window fit the stage
     auto dma_tick = [&](int t) {
         const float* src = g.pcm + (int64_t)s * g.stride + (int64_t)t * g.tick_stride;
+        if (DMA == 2) {   // 16-B pieces (1 KiB per wave-instruction): tick rows 16-B aligned, block % 4 == 0
+            for (int c0 = 0; c0 < ((EWK_GATE_ABLATE & 4) ? 0 : fs); c0 += 256) {
+                if (c0 + 4 * lane < fs)
+                    __builtin_amdgcn_global_load_lds(src + c0 + 4 * lane,
+                                                     (__attribute__((address_space(3))) void*)(stage + c0), 16, 0, 0);
+            }
+            return;
+        }
         for (int c0 = 0; c0 < fs; c0 += 64) {
             if (c0 + lane < fs)
                 __builtin_amdgcn_global_load_lds(src + c0 + lane, (__attribute__((address_space(3))) void*)(stage + c0),
@@ -469,7 +481,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
         // chunks of kIngestLoads loads per lane in flight before any store (the ring may
         // alias the input as far as the compiler knows: a load-store loop serialises them);
         // chunk 0 of this tick was requested before the previous tick's compute
-        if (dma) {   // this tick's samples landed in the stage: ring stores from LDS
+        if (DMA == 2) {   // 16-B ring stores from the stage (ring rows and p0 4-float aligned: no group wraps)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wave_sync();
+            float4 xv[kDma4Chunks];
+#pragma unroll
+            for (int c = 0; c < kDma4Chunks; ++c) {
+                const int i = 256 * c + 4 * lane;
+                xv[c] = i < fs ? *reinterpret_cast<const float4*>(stage + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int c = 0; c < kDma4Chunks; ++c) {
+                const int i = 256 * c + 4 * lane;
+                if (i < fs && !(EWK_GATE_ABLATE & 2)) {
+                    int k = p0 + i;
+                    if (k >= R) k -= R;
+                    *reinterpret_cast<float4*>(ring + k) = xv[c];
+                }
+            }
+        } else if (dma) {   // this tick's samples landed in the stage: ring stores from LDS
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             wave_sync();
             for (int c0 = 0; c0 < fs; c0 += 64 * kIngestLoads) {
@@ -519,7 +549,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
         double reuse_sum = 0.0;
         bool have_reuse = false;
         // ---- a2: threshold over the physical blocks (only once the ring is full)
-        if (full) {
+        if (full && !(EWK_GATE_ABLATE & 1)) {
             auto block_sum = [&](int b) -> double {
                 const int a0 = b * fs;
                 if (staged && a0 == p0)   // the block is exactly this tick's samples
@@ -725,11 +755,17 @@ hipError_t launch_gate(const GateArgs& g, hipStream_t s) {
     const size_t lds = 4 * per_wave;
     const int64_t nl = std::min<int64_t>(g.n_last, g.ring_len);
     const bool dma = EWK_GATE_DMA && g.pcm16 == nullptr && g.stage >= g.block && g.stage >= nl;
+    // 16-B pieces: every tick row 16-B aligned, whole 4-sample groups that never straddle the ring wrap
+    const bool dma4 = dma && EWK_GATE_DMA >= 2 && g.block % 4 == 0 && g.block <= 256 * kDma4Chunks &&
+                      g.stride % 4 == 0 && g.tick_stride % 4 == 0 && g.ring_len % 4 == 0 &&
+                      ((uintptr_t)g.pcm & 15) == 0;
     if (g.n_blocks <= 128) {
-        if (dma) hipLaunchKernelGGL((k_gate_ticks<2, 1>), dim3(grid), dim3(256), lds, s, g);
+        if (dma4) hipLaunchKernelGGL((k_gate_ticks<2, 2>), dim3(grid), dim3(256), lds, s, g);
+        else if (dma) hipLaunchKernelGGL((k_gate_ticks<2, 1>), dim3(grid), dim3(256), lds, s, g);
         else hipLaunchKernelGGL((k_gate_ticks<2, 0>), dim3(grid), dim3(256), lds, s, g);
     } else if (g.n_blocks <= 64 * kGateRegMax) {
-        if (dma) hipLaunchKernelGGL((k_gate_ticks<kGateRegMax, 1>), dim3(grid), dim3(256), lds, s, g);
+        if (dma4) hipLaunchKernelGGL((k_gate_ticks<kGateRegMax, 2>), dim3(grid), dim3(256), lds, s, g);
+        else if (dma) hipLaunchKernelGGL((k_gate_ticks<kGateRegMax, 1>), dim3(grid), dim3(256), lds, s, g);
         else hipLaunchKernelGGL((k_gate_ticks<kGateRegMax, 0>), dim3(grid), dim3(256), lds, s, g);
     } else {
         hipLaunchKernelGGL((k_gate_ticks<0, 0>), dim3(grid), dim3(256), lds, s, g);
