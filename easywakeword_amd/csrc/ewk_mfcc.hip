@@ -645,31 +645,51 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
         float* pB0 = scf - rowA;                     // P[256-k]  at pB0[256 - 16 it]
         float* pB1 = z0 ? scf + 136 : pB0;
         float* pB2 = z0 ? scf + 136 : pB0 + 16;
+        // two steps per iteration, their stores grouped by base (pa, pa, pb, pb) so that
+        // the stores of consecutive steps merge into ds_write2_b32
 #pragma unroll
-        for (int it = 0; it < 17; ++it) {
-            const float2 w = tw[it];   // (cos, sin)(2 pi k / 512)
-            const float2 ug = b[0][dperm(it < 16 ? it : 15)];
-            const float2 vg = b[1][dperm(it < 16 ? 15 - it : 0)];
-            float2 u, vv;
-            if (it <= 8) {
-                u = ug;
-                const float2 vz = b[0][dperm((16 - it) & 15)];
-                vv = z0 ? vz : vg;
-            } else {
-                const float2 uz = b[1][dperm(it - 9)], vz = b[1][dperm(24 - it)];
-                u = z0 ? uz : ug;
-                vv = z0 ? vz : vg;
+        for (int it0 = 0; it0 < 17; it0 += 2) {
+            float py[2], px[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int it = it0 + u;
+                if (it >= 17) break;
+                const float2 w = tw[it];   // (cos, sin)(2 pi k / 512)
+                const float2 ug = b[0][dperm(it < 16 ? it : 15)];
+                const float2 vg = b[1][dperm(it < 16 ? 15 - it : 0)];
+                float2 uu, vv;
+                if (it <= 8) {
+                    uu = ug;
+                    const float2 vz = b[0][dperm((16 - it) & 15)];
+                    vv = z0 ? vz : vg;
+                } else {
+                    const float2 uz = b[1][dperm(it - 9)], vz = b[1][dperm(24 - it)];
+                    uu = z0 ? uz : ug;
+                    vv = z0 ? vz : vg;
+                }
+                const float ar = uu.x + vv.x, ai = uu.y - vv.y;
+                const float br = uu.x - vv.x, bi = uu.y + vv.y;
+                const float cr = w.y * br - w.x * bi;
+                const float ci = w.y * bi + w.x * br;
+                const float yr = ar - cr, yi = ai - ci;
+                const float xr = ar + cr, xi = ai + ci;
+                py[u] = yr * yr + yi * yi;
+                px[u] = xr * xr + xi * xi;
             }
-            const float ar = u.x + vv.x, ai = u.y - vv.y;
-            const float br = u.x - vv.x, bi = u.y + vv.y;
-            const float cr = w.y * br - w.x * bi;
-            const float ci = w.y * bi + w.x * br;
-            const float yr = ar - cr, yi = ai - ci;
-            const float xr = ar + cr, xi = ai + ci;
-            float* pa = it <= 8 ? pA0 : (it < 16 ? pA1 : pA2);
-            float* pb = it <= 8 ? pB0 : (it < 16 ? pB1 : pB2);
-            pa[16 * it] = yr * yr + yi * yi;
-            pb[256 - 16 * it] = xr * xr + xi * xi;
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int it = it0 + u;
+                if (it >= 17) break;
+                float* pa = it <= 8 ? pA0 : (it < 16 ? pA1 : pA2);
+                pa[16 * it] = py[u];
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int it = it0 + u;
+                if (it >= 17) break;
+                float* pb = it <= 8 ? pB0 : (it < 16 ? pB1 : pB2);
+                pb[256 - 16 * it] = px[u];
+            }
         }
         // the zero pad (bins 257..271) the unrolled band loops read past bin 256
         scf[257 + jp] = 0.0f;
