@@ -271,7 +271,7 @@ __device__ __forceinline__ double percentile25_sorted(const double* sorted, int 
 #define EWK_GATE_DMA 2   // float32 tick ingest by LDS-DMA (0: register chunks, 1: 4-B pieces, 2: 16-B pieces when aligned)
 #endif
 #ifndef EWK_GATE_WPE
-#define EWK_GATE_WPE 2   // min waves per SIMD the register allocator must allow (4 spills: measured slower)
+#define EWK_GATE_WPE 4   // min waves per SIMD the register allocator must allow (121 VGPRs; 5 spills and runs 37 % slower)
 #endif
 constexpr int kDma4Chunks = 8;     // 16-B DMA path: ticks of up to 8 * 256 samples copied to the ring in one batch
 constexpr int kIngestLoads = 4;    // tick samples per lane loaded ahead of the ring stores (16: 166 VGPRs, 3 waves/SIMD, 10 % slower)
@@ -484,20 +484,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
         if (DMA == 2) {   // 16-B ring stores from the stage (ring rows and p0 4-float aligned: no group wraps)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             wave_sync();
-            float4 xv[kDma4Chunks];
 #pragma unroll
-            for (int c = 0; c < kDma4Chunks; ++c) {
-                const int i = 256 * c + 4 * lane;
-                xv[c] = i < fs ? *reinterpret_cast<const float4*>(stage + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-            }
+            for (int h = 0; h < kDma4Chunks; h += 4) {   // batches of 4 (16 VGPRs)
+                float4 xv[4];
 #pragma unroll
-            for (int c = 0; c < kDma4Chunks; ++c) {
-                const int i = 256 * c + 4 * lane;
-                if (i < fs && !(EWK_GATE_ABLATE & 2)) {
-                    int k = p0 + i;
-                    if (k >= R) k -= R;
-                    *reinterpret_cast<float4*>(ring + k) = xv[c];
+                for (int c = 0; c < 4; ++c) {
+                    const int i = 256 * (h + c) + 4 * lane;
+                    xv[c] = i < fs ? *reinterpret_cast<const float4*>(stage + i) : make_float4(0.f, 0.f, 0.f, 0.f);
                 }
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int i = 256 * (h + c) + 4 * lane;
+                    if (i < fs && !(EWK_GATE_ABLATE & 2)) {
+                        int k = p0 + i;
+                        if (k >= R) k -= R;
+                        *reinterpret_cast<float4*>(ring + k) = xv[c];
+                    }
+                }
+                if (256 * (h + 4) >= fs) break;
             }
         } else if (dma) {   // this tick's samples landed in the stage: ring stores from LDS
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
