@@ -703,9 +703,13 @@ static int score_pending(ewk_engine* e, hipStream_t ss, const int32_t* n_events)
     const int64_t per = (1 + e->ring_len / HOP) * (NMEL + NMFCC);
     {
         ProfScope ps(e, 1, ss);
+        // the re-score launch also advances the watermark (its last workgroup: k_advance folded in)
+        a.adv_done = e->d_work + 3;
+        a.adv_ev_base = e->evc_bank(e->bank) + 2;
         HIP_TRY(launch_score_f64(e->d_tab64, a, 1, e->f64_scratch.p, per, e->f64_grid, nullptr, nullptr, ss));
     }
-    HIP_TRY(launch_advance_watermark(e->evc_bank(e->bank) + 2, n_events, e->d_work + 1, e->d_work + 2, ss));
+    if (e->f64_grid <= 0)
+        HIP_TRY(launch_advance_watermark(e->evc_bank(e->bank) + 2, n_events, e->d_work + 1, e->d_work + 2, ss));
     return EWK_OK;
 }
 

@@ -94,6 +94,10 @@ struct ScoreArgs {
     float2* lm_scratch;       // per-wave parked log-mel tiles for the top_db clamp pass
     int32_t lm_tiles;         // tiles per wave in lm_scratch
     int32_t* order;           // linear mode: work order scratch [n_seg] (longest first), nullptr = index order
+    // ring mode, k_score_f64: the last workgroup sets *adv_ev_base = *n_events and zeroes
+    // *work, *rescore_count (and *adv_done); nullptr = no watermark advance
+    int32_t* adv_done;
+    int32_t* adv_ev_base;
 };
 
 hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mode, hipStream_t s);

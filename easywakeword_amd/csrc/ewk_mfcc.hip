@@ -1755,24 +1755,13 @@ __device__ void fft256_f64(double2* z, const double2* tw, int lane) {
 // FFT, packed-support mel, log10), then the workgroup clamps at max - 80 dB, runs the
 // fp64 DCT and numpy's pairwise mean / population std.
 template <int RING>
-__global__ __launch_bounds__(256) void k_score_f64(const Tables64* __restrict__ tb, ScoreArgs a,
-                                                   double* scratch, int64_t per_seg,
-                                                   double* out_mean64, double* out_std64) {
-    __shared__ double2 s_z[4][256];
-    __shared__ double s_p[4][NBIN + 3];
-    __shared__ double s_win[NFFT];
-    __shared__ double2 s_tw[128];          // W256^k
-    __shared__ double2 s_cs[NBIN];         // (cos, sin)(2 pi k / 512), k <= 256
-    __shared__ double s_dct[NMFCC * NMEL];
-    __shared__ float s_mw[2 * NBIN + 2 * NMEL];
-    __shared__ int s_mlo[NMEL], s_moff[NMEL + 1];
-    __shared__ double s_red[4];
-    __shared__ double s_stat[2 * NMFCC];
+__device__ __forceinline__ void score_f64_body(const Tables64* __restrict__ tb, const ScoreArgs& a, double* scratch,
+                                               int64_t per_seg, double* out_mean64, double* out_std64, int count,
+                                               double2 (&s_z)[4][256], double (&s_p)[4][NBIN + 3], double (&s_win)[NFFT],
+                                               double2 (&s_tw)[128], double2 (&s_cs)[NBIN], double (&s_dct)[NMFCC * NMEL],
+                                               float (&s_mw)[2 * NBIN + 2 * NMEL], int (&s_mlo)[NMEL],
+                                               int (&s_moff)[NMEL + 1], double (&s_red)[4], double (&s_stat)[2 * NMFCC]) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    int count;
-    if (a.rescore_list) count = min(*a.rescore_count, a.rescore_cap);
-    else count = RING ? min(a.n_seg, *a.n_events) : a.n_seg;
-    if ((int)blockIdx.x >= count) return;   // nothing for this workgroup (the common case per tick)
     for (int i = tid; i < NFFT; i += 256) s_win[i] = tb->win[i];
     for (int i = tid; i < 128; i += 256) s_tw[i] = make_double2(tb->cs[2 * i], -tb->sn[2 * i]);   // W256^i = W512^2i
     for (int i = tid; i < NBIN; i += 256) s_cs[i] = make_double2(tb->cs[i], tb->sn[i]);
@@ -1884,6 +1873,42 @@ __global__ __launch_bounds__(256) void k_score_f64(const Tables64* __restrict__ 
     }
 }
 
+template <int RING>
+__global__ __launch_bounds__(256) void k_score_f64(const Tables64* __restrict__ tb, ScoreArgs a,
+                                                   double* scratch, int64_t per_seg,
+                                                   double* out_mean64, double* out_std64) {
+    __shared__ double2 s_z[4][256];
+    __shared__ double s_p[4][NBIN + 3];
+    __shared__ double s_win[NFFT];
+    __shared__ double2 s_tw[128];          // W256^k
+    __shared__ double2 s_cs[NBIN];         // (cos, sin)(2 pi k / 512), k <= 256
+    __shared__ double s_dct[NMFCC * NMEL];
+    __shared__ float s_mw[2 * NBIN + 2 * NMEL];
+    __shared__ int s_mlo[NMEL], s_moff[NMEL + 1];
+    __shared__ double s_red[4];
+    __shared__ double s_stat[2 * NMFCC];
+    int count;
+    if (a.rescore_list) count = min(*a.rescore_count, a.rescore_cap);
+    else count = RING ? min(a.n_seg, *a.n_events) : a.n_seg;
+    if ((int)blockIdx.x < count) score_f64_body<RING>(tb, a, scratch, per_seg, out_mean64, out_std64, count,
+                                                        s_z, s_p, s_win, s_tw, s_cs, s_dct, s_mw, s_mlo, s_moff,
+                                                        s_red, s_stat);
+    // ring mode: the last workgroup out advances the watermark and re-arms the counters
+    // (k_advance folded in: one launch fewer per tick)
+    if (a.adv_done) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            if (atomicAdd(a.adv_done, 1) == (int)gridDim.x - 1) {
+                *a.adv_ev_base = *a.n_events;
+                *a.work = 0;
+                *a.rescore_count = 0;
+                *a.adv_done = 0;
+                __threadfence();
+            }
+        }
+    }
+}
 hipError_t launch_score_f64(const Tables64* d_tab64, const ScoreArgs& a, int ring_mode, double* d_scratch,
                             int64_t scratch_per_seg, int grid, double* out_mean64, double* out_std64,
                             hipStream_t s) {
