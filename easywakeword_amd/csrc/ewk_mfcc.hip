@@ -47,6 +47,10 @@
 #define EWK_ADDTID_STAGE 1   // sample staging with ds_write_addtid_b32 (0: ds_write_b32)
 #endif
 
+#ifndef EWK_PRIO
+#define EWK_PRIO 2   // s_setprio 1 over the frame-pass LDS phases (window, transposes, mel): -0.4 %; 1 = VALU phases high: +1 %
+#endif
+#define EWK_SETPRIO(v) __builtin_amdgcn_s_setprio(v)
 #ifndef EWK_TIMING
 #define EWK_TIMING 0   // per-phase s_memtime accounting (scripts/mb_score.py variants only)
 #endif
@@ -409,6 +413,9 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
                                            const unsigned char* smem, float* scr, float* tile,
                                            int lane, const int (&lo)[8], float& vmax, float& vmin,
                                            float clampv = -INFINITY, uint64_t* tim = nullptr) {
+#if EWK_PRIO == 2
+    EWK_SETPRIO(1);
+#endif
     EWK_TS(p0);
     // lane group f = lane>>4 holds frames fr = 4 g + f (g < kNF) of this pass; the
     // kNF frames of a lane are independent instruction streams (ILP for the wave).
@@ -462,6 +469,9 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
         }
         EWK_TS(p1);
         if (tim) EWK_TACC(8, p0, p1);
+#if EWK_PRIO
+        EWK_SETPRIO(EWK_PRIO == 1 ? 1 : 0);
+#endif
         // ---- DFT16 over n1 (window folded into its first stage), twiddle W256^(j*k1)
         // (one twiddle row serves every frame of the lane, requested before the DFT16s)
         EWK_LD128_8(t4, (uint32_t)(uintptr_t)(reinterpret_cast<const float4*>(smem + L_TW1) + j * (TP / 2)));
@@ -489,6 +499,9 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
             }
         }
     }
+#if EWK_PRIO
+    EWK_SETPRIO(EWK_PRIO == 1 ? 0 : 1);
+#endif
     EWK_TS(p3);
     if (tim) EWK_TACC(10, p2, p3);
     // ---- transpose through LDS (real, then imaginary half): lane k1 <- A_{n2}[k1].
@@ -609,6 +622,9 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
             lds_order();
         }
     }
+#endif
+#if EWK_PRIO
+    EWK_SETPRIO(EWK_PRIO == 1 ? 1 : 0);
 #endif
     EWK_TS(p4);
     if (tim) EWK_TACC(11, p3, p4);
@@ -735,6 +751,9 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     }
 #endif
     lds_order();
+#if EWK_PRIO
+    EWK_SETPRIO(EWK_PRIO == 1 ? 0 : 1);
+#endif
     EWK_TS(p6);
     if (tim) EWK_TACC(13, p5, p6);
     if (next) stage_load(v, (t0 + kFPP) * HOP - NFFT / 2, lane, pf);
@@ -782,6 +801,9 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
                 }
         }
     }
+#if EWK_PRIO == 2
+    EWK_SETPRIO(0);
+#endif
     EWK_TS(p7);
     if (tim) EWK_TACC(14, p6, p7);
     lds_order();
@@ -1425,6 +1447,15 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, fl
 template <int RING>
 __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const Tables* __restrict__ tab, ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    // ring mode: the event window and this workgroup's first event, requested before the
+    // table fill so their latency overlaps it
+    int r_base = 0, r_count = 0;
+    ewk_event r_ev = {};
+    if (RING) {
+        r_base = *a.ev_base;
+        r_count = min(*a.n_events, a.n_seg) - r_base;
+        if ((int)blockIdx.x < r_count) r_ev = a.events[r_base + blockIdx.x];
+    }
     // ---- cooperative table load (global -> LDS), per-lane rows transposed
     {
         float2* sw2 = reinterpret_cast<float2*>(smem + L_WIN2);
@@ -1488,8 +1519,8 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int base = 0, count = a.n_seg;
     if (RING) {
-        base = *a.ev_base;
-        count = min(*a.n_events, a.n_seg) - base;
+        base = r_base;
+        count = r_count;
     }
     unsigned char* wbase = smem + L_SHARED_END + wave * W_BYTES;
     float* scr = reinterpret_cast<float*>(smem + L_SCR + wave * SCR_BYTES);
@@ -1517,14 +1548,13 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
     if (RING) {   // one segment per workgroup at a time, its tiles spread over the waves
         int* wg_idx = reinterpret_cast<int*>(smem + L_WG);
         float* misc0 = reinterpret_cast<float*>(smem + L_SCR);   // wave 0's FFT scratch (epilogue only)
-        for (;;) {
-            if (threadIdx.x == 0) wg_idx[0] = atomicAdd(a.work, 1);
-            __syncthreads();
-            const int idx = wg_idx[0];
-            __syncthreads();
-            if (idx >= count) break;
+        (void)wg_idx;
+        // static assignment (a tick's few hundred segments are about one per workgroup);
+        // the first event was requested before the table fill
+        for (int idx = blockIdx.x; idx < count; idx += gridDim.x) {
+            __syncthreads();   // wave 0's scratch (misc0) is free again
             const int seg = base + idx;
-            const ewk_event ev = a.events[seg];
+            const ewk_event ev = idx == (int)blockIdx.x ? r_ev : a.events[seg];
             if (ev.flags & EWK_EV_SKIPPED) continue;
             const SegSrc<RING> v = make_src<RING>(a.pcm + (int64_t)ev.stream * a.ring_len, ev.ring_start,
                                                   a.ring_len, ev.length);
