@@ -42,6 +42,9 @@
 #ifndef EWK_GATE_ABLATE
 #define EWK_GATE_ABLATE 0   // timing-only ablations (scripts/mb_gate.py): 1 no a2, 2 no ring stores, 4 no tick loads
 #endif
+#ifndef EWK_GATE_GRID_MAX
+#define EWK_GATE_GRID_MAX 1024   // workgroups of 4 waves: 256 CUs x 16 waves (4 waves/SIMD)
+#endif
 #ifndef EWK_GATE_TIMING
 #define EWK_GATE_TIMING 0   // per-phase s_memtime accounting (scripts/mb_gate.py variants only)
 #endif
@@ -391,8 +394,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const PwTree* __restrict__ trees = g.trees;   // read-only, cache-resident
-    const int s = blockIdx.x * 4 + wave;
+    // persistent over streams: wave w takes streams w, w + waves-in-grid, ...; the next
+    // stream's first tick is requested (LDS-DMA) as soon as this stream's last tick has
+    // issued its stage reads, so its HBM latency overlaps this stream's FSM and stores
+    int s = blockIdx.x * 4 + wave;
     if (s >= g.n_streams) return;
+    const int wstride = (int)gridDim.x * 4;
     const size_t per_wave = (size_t)g.val_len * 8 + (size_t)g.stage * 4;
     unsigned char* w = smem + wave * per_wave;
     double* val = reinterpret_cast<double*>(w);
@@ -402,7 +409,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
     const int fs = g.block;
     const int nb = g.n_blocks;
     const int nl = (int)min<int64_t>(g.n_last, g.ring_len);
-    float* ring = g.ring + (int64_t)s * R;
     // the first tick's samples are requested before the state: no load waits on another
     float xin[kIngestLoads];
     auto load_chunk = [&](int t, int c0) {
@@ -423,8 +429,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
     // trip per tick instead of one per register chunk
     const bool staged = g.stage >= fs && g.stage >= nl;
     constexpr bool dma = DMA != 0;   // launch_gate: float32 input, tick and window fit the stage
-    auto dma_tick = [&](int t) {
-        const float* src = g.pcm + (int64_t)s * g.stride + (int64_t)t * g.tick_stride;
+    auto dma_tick = [&](int ss, int t) {
+        const float* src = g.pcm + (int64_t)ss * g.stride + (int64_t)t * g.tick_stride;
         if (DMA == 2) {   // 16-B pieces (1 KiB per wave-instruction): tick rows 16-B aligned, block % 4 == 0
             for (int c0 = 0; c0 < ((EWK_GATE_ABLATE & 4) ? 0 : fs); c0 += 256) {
                 if (c0 + 4 * lane < fs)
@@ -439,8 +445,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
                                                  4, 0, 0);
         }
     };
-    if (dma) dma_tick(0);
+    if (dma) dma_tick(s, 0);
     else load_chunk(0, 0);
+    for (;;) {
+    float* ring = g.ring + (int64_t)s * R;
     GateStream st = g.st[s];
     double* grms = g.block_rms + (int64_t)s * nb;
     double* sorted2 = g.sorted_rms + (int64_t)s * 2 * nb;
@@ -647,7 +655,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
         }
         if (dma && t + 1 < g.n_ticks) {   // the stage's last reader (a3) has issued its reads
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            dma_tick(t + 1);
+            dma_tick(s, t + 1);
+        } else if (dma && s + wstride < g.n_streams) {   // last tick: the next stream's first
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            dma_tick(s + wstride, 0);
         }
         GT_TS(q3);
         GT_ACC(3, q2, q3);
@@ -734,6 +745,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
         }
     }
     if (lane == 0) g.st[s] = st;
+    s += wstride;
+    if (s >= g.n_streams) break;
+    if (!dma) load_chunk(0, 0);
+    }
 #if EWK_GATE_TIMING
     GT_TS(q_end);
     GT_ACC(5, q_loop, q_end);
@@ -754,7 +769,9 @@ int gate_val_len(const PwTree* trees_host, int n_blocks) {
 
 hipError_t launch_gate(const GateArgs& g, hipStream_t s) {
     if (g.n_streams <= 0 || g.n_ticks <= 0) return hipSuccess;
-    const int grid = (g.n_streams + 3) / 4;
+    // at most one resident wave per stream slot (16 waves/CU at 4 waves/SIMD); more
+    // streams loop inside the waves
+    const int grid = std::min((g.n_streams + 3) / 4, EWK_GATE_GRID_MAX);
     const size_t per_wave = (size_t)g.val_len * 8 + (size_t)g.stage * 4;
     const size_t lds = 4 * per_wave;
     const int64_t nl = std::min<int64_t>(g.n_last, g.ring_len);
