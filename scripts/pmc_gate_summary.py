@@ -16,7 +16,8 @@ def main():
     d = sys.argv[1]
     n_streams = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
     print(f"streaming-kernel PMC summary ({d}), {n_streams} streams, one tick per launch")
-    for kern, grid in (("k_gate_ticks", n_streams * 64), ("k_score_f32<1>", None)):
+    # the gate grid is capped at 1024 workgroups of 4 waves (EWK_GATE_GRID_MAX); more streams loop in-wave
+    for kern, grid in (("k_gate_ticks", min(n_streams, 4096) * 64), ("k_score_f32<1>", None)):
         agg = collections.defaultdict(list)
         durs = []
         for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
