@@ -52,7 +52,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--streams", type=int, default=1024, help="streams per GPU (config 2)")
     ap.add_argument("--segments-per-stream", type=int, default=64)
     ap.add_argument("--seed", type=int, default=1234)

@@ -14,16 +14,16 @@ if [ "$MODE" = all ] || [ "$MODE" = test ]; then
   ok_or_testfail $rc || exit $rc
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
-  timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.log 2>&1
+  timeout -k 10 600 python bench.py --steps 20 --warmup 10 > gpurun_out/bench.log 2>&1
   rc=$?; echo "bench rc=$rc"; tail -c 3000 gpurun_out/bench.log
   [ $rc -eq 0 ] || exit $rc
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   cd /tmp && export TMPDIR=/tmp
   R="${GRAFT_REPO_ROOT:-/root/repo}"
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline --fixed-len 0 > "$R/gpurun_out/prof.log" 2>&1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 20 --warmup 10 --no-cpu-baseline --fixed-len 0 > "$R/gpurun_out/prof.log" 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -5 "$R/gpurun_out/prof.log"
-  python "$R/scripts/prof_summary.py" "$R/gpurun_out/prof" 1 > "$R/gpurun_out/kernel_stats.txt" 2>&1
+  python "$R/scripts/prof_summary.py" "$R/gpurun_out/prof" 10 > "$R/gpurun_out/kernel_stats.txt" 2>&1
   rm -f "$R/gpurun_out/prof/run_kernel_trace.csv"   # large; the stats csv and the summary stay
 fi
 if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then
