@@ -169,3 +169,35 @@ def test_longest_first_order_is_bit_identical(engine):
     np.testing.assert_array_equal(s1, s2)
     np.testing.assert_array_equal(sc1, sc2)     # NaN == NaN in assert_array_equal
     np.testing.assert_array_equal(mt1, mt2)
+
+
+def test_speculative_top_db_clamp(engine):
+    """Pass 1 clamps each 16-frame tile at the running segment max - 80 dB
+    (top_db).  A loud burst placed in the last tile forces
+    every earlier (quiet) tile through the parked fix-up; one in the first tile
+    makes every later tile exact in pass 1; a burst mid-way mixes both.  All must
+    equal the oracle, and a quiet tail after the burst must not be clamped at a
+    stale threshold."""
+    engine.template_from_pcm(synth.load_word())
+    tm, ts = engine.get_template()
+    rng = np.random.Generator(np.random.PCG64(5))
+    word = synth.load_word()
+    segs = []
+    for L in (16000, 30000, 47000):
+        for where in (0.0, 0.5, 1.0):
+            x = rng.normal(0, 1e-5, L).astype(np.float32)   # ~ -100 dB floor, far below max - 80
+            w = word[: min(len(word), L // 3)] * np.float32(3.0)
+            s0 = int(where * (L - len(w)))
+            x[s0:s0 + len(w)] += w
+            segs.append(x)
+        # loud 880 Hz tone in the last 0.2 s only: every earlier tile is fixed up
+        t = np.arange(3200) / 16000
+        y = rng.normal(0, 1e-4, L).astype(np.float32)
+        y[-3200:] += (0.9 * np.sin(2 * np.pi * 880 * t)).astype(np.float32)
+        segs.append(y)
+    _, _, score, match = engine.score(segs, candidate_dtype="float64")
+    for i, x in enumerate(segs):
+        cm, cs = mfcc_ref.extract_mfcc(x.astype(np.float64))
+        ref = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
+        assert score_close(score[i], ref, SCORE_TOL), (i, len(x), score[i], ref)
+        assert bool(match[i]) == (ref >= 75.0)
