@@ -77,7 +77,19 @@ constexpr int kStageLoads = ((kFPP - 1) * HOP + NFFT + 63) / 64;   // dword load
 // frame fr's FFT scratch starts at fr * 272 + 8 * (fr >> 2): the two frames a 16-lane
 // group untangles side by side (fr, fr + 4) land 8 banks apart
 constexpr int kScrFrames = kFPP * SCR_FRAME + 8 * (kNF - 1);
-constexpr int kScrFloats = (kScrFrames > 64 * kStageLoads) ? kScrFrames : 64 * kStageLoads;
+// kNF = 2: a lane's two frames are consecutive (slot (g, f) = frame 2f + g of the pass),
+// so the second frame's first 11 sample pairs are the first frame's pairs 5..15 (hop 160 =
+// 5 x 32) and only 5 more are read.  The stage is skewed -- sample s at s + 32 floor(s / 320)
+// -- so the four lane groups' frames (320 samples apart) land 32 banks apart.
+#ifndef EWK_FPAIR
+#define EWK_FPAIR (EWK_NF == 2)
+#endif
+__host__ __device__ constexpr int stg_off(int c) { return 256 * c + (EWK_FPAIR ? 128 * (c / 5) : 0); }   // bytes of stage row c
+__host__ __device__ constexpr int win_off(int g, int n1) {   // bytes: pair n1 of slot g from the lane's base
+    return 4 * (160 * g + 32 * n1 + 32 * ((160 * g + 32 * n1) / 320));
+}
+constexpr int kStageFloats = stg_off(kStageLoads) / 4;
+constexpr int kScrFloats = (kScrFrames > kStageFloats) ? kScrFrames : kStageFloats;
 // The per-wave FFT scratch (also the sample staging) comes first in LDS: the M0 base of
 // ds_write_addtid_b32 is 16 bits wide, so every wave's scratch must start below 64 KB.
 constexpr int SCR_BYTES = (kScrFloats * 4 + 15) & ~15;
@@ -375,11 +387,11 @@ __device__ __forceinline__ void stage_load(const SegSrc<RING>& v, int q0, int la
                  : [base] "s"(m0base), [r0] "v"(r[o]), [r1] "v"(r[o + 1]), [r2] "v"(r[o + 2]), [r3] "v"(r[o + 3]), \
                    [r4] "v"(r[o + 4]), [r5] "v"(r[o + 5]), [r6] "v"(r[o + 6]), [r7] "v"(r[o + 7]),                \
                    [r8] "v"(r[o + 8]), [r9] "v"(r[o + 9]), [r10] "v"(r[o + 10]), [r11] "v"(r[o + 11]),          \
-                   [r12] "v"(r[o + 12]), [o0] "i"(256 * (o)), [o1] "i"(256 * (o + 1)), [o2] "i"(256 * (o + 2)), \
-                   [o3] "i"(256 * (o + 3)), [o4] "i"(256 * (o + 4)), [o5] "i"(256 * (o + 5)),                    \
-                   [o6] "i"(256 * (o + 6)), [o7] "i"(256 * (o + 7)), [o8] "i"(256 * (o + 8)),                    \
-                   [o9] "i"(256 * (o + 9)), [o10] "i"(256 * (o + 10)), [o11] "i"(256 * (o + 11)),                \
-                   [o12] "i"(256 * (o + 12))                                                                     \
+                   [r12] "v"(r[o + 12]), [o0] "i"(stg_off(o)), [o1] "i"(stg_off(o + 1)), [o2] "i"(stg_off(o + 2)), \
+                   [o3] "i"(stg_off(o + 3)), [o4] "i"(stg_off(o + 4)), [o5] "i"(stg_off(o + 5)),                    \
+                   [o6] "i"(stg_off(o + 6)), [o7] "i"(stg_off(o + 7)), [o8] "i"(stg_off(o + 8)),                    \
+                   [o9] "i"(stg_off(o + 9)), [o10] "i"(stg_off(o + 10)), [o11] "i"(stg_off(o + 11)),                \
+                   [o12] "i"(stg_off(o + 12))                                                                     \
                  : "memory")
 static_assert(kStageLoads == 26, "stage_store writes two blocks of 13 rows");
 #endif
@@ -391,7 +403,7 @@ __device__ __forceinline__ void stage_store(float* stage, int lane, const float 
     EWK_ST13(13);
 #else
 #pragma unroll
-    for (int c = 0; c < kStageLoads; ++c) stage[64 * c + lane] = r[c];
+    for (int c = 0; c < kStageLoads; ++c) stage[stg_off(c) / 4 + lane] = r[c];
 #endif
 }
 
@@ -431,7 +443,7 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     float* sc[kNF];
 #pragma unroll
     for (int g = 0; g < kNF; ++g) {
-        valid[g] = t0 + 4 * g + f < T;
+        valid[g] = t0 + (EWK_FPAIR ? 2 * f + g : 4 * g + f) < T;
         sc[g] = scr + (4 * g + f) * SCR_FRAME + 8 * g;
     }
 
@@ -442,6 +454,17 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     floatx4 t4[8];   // twiddle row W256^(j*k1)
     {
         float2 x[kNF][16];
+#if EWK_FPAIR
+        {
+            const uint32_t sa = (uint32_t)(uintptr_t)(scr + 352 * f + 2 * j);
+#define EWK_LD64(g, n) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(x[g][n]) : "v"(sa), "i"(win_off(g, n)) : "memory")
+            EWK_LD64(0, 0); EWK_LD64(0, 1); EWK_LD64(0, 2); EWK_LD64(0, 3); EWK_LD64(0, 4); EWK_LD64(0, 5);
+            EWK_LD64(0, 6); EWK_LD64(0, 7); EWK_LD64(0, 8); EWK_LD64(0, 9); EWK_LD64(0, 10); EWK_LD64(0, 11);
+            EWK_LD64(0, 12); EWK_LD64(0, 13); EWK_LD64(0, 14); EWK_LD64(0, 15);
+            EWK_LD64(1, 11); EWK_LD64(1, 12); EWK_LD64(1, 13); EWK_LD64(1, 14); EWK_LD64(1, 15);
+#undef EWK_LD64
+        }
+#else
 #pragma unroll
         for (int g = 0; g < kNF; ++g) {
             const uint32_t sa = (uint32_t)(uintptr_t)(scr + (4 * g + f) * HOP + 2 * j);
@@ -450,9 +473,24 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
             EWK_LD64(8); EWK_LD64(9); EWK_LD64(10); EWK_LD64(11); EWK_LD64(12); EWK_LD64(13); EWK_LD64(14); EWK_LD64(15);
 #undef EWK_LD64
         }
+#endif
         floatx4 w4[8];   // this lane's window pairs, fetched in the same batch
         EWK_LD128_8(w4, (uint32_t)(uintptr_t)(reinterpret_cast<const float4*>(smem + L_WIN2) + j * (TP / 2)));
         EWK_WAIT_8(w4);
+#if EWK_FPAIR
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(x[0][0]), "+v"(x[0][1]), "+v"(x[0][2]), "+v"(x[0][3]), "+v"(x[0][4]), "+v"(x[0][5]),
+                       "+v"(x[0][6]), "+v"(x[0][7]), "+v"(x[0][8]), "+v"(x[0][9]), "+v"(x[0][10]), "+v"(x[0][11]),
+                       "+v"(x[0][12]), "+v"(x[0][13]), "+v"(x[0][14]), "+v"(x[0][15])
+                     :
+                     : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(x[1][11]), "+v"(x[1][12]), "+v"(x[1][13]), "+v"(x[1][14]), "+v"(x[1][15])
+                     :
+                     : "memory");
+#pragma unroll
+        for (int n = 0; n <= 10; ++n) x[1][n] = x[0][n + 5];   // the shared sample pairs
+#else
 #pragma unroll
         for (int g = 0; g < kNF; ++g)
             asm volatile("s_waitcnt lgkmcnt(0)"
@@ -461,6 +499,7 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
                            "+v"(x[g][12]), "+v"(x[g][13]), "+v"(x[g][14]), "+v"(x[g][15])
                          :
                          : "memory");
+#endif
         float2 wv[16];
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
@@ -813,7 +852,7 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     // k-chunk j of its frame row (hi and lo halves, one ds_write_b128 each).
 #pragma unroll
     for (int g = 0; g < kNF; ++g) {
-        const int r = row0 + 4 * g + f;
+        const int r = row0 + (EWK_FPAIR ? 2 * f + g : 4 * g + f);
         float fmx = db[g][0], fmn = db[g][0], x[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
