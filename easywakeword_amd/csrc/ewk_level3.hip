@@ -122,10 +122,19 @@ struct L3Src {
     }
 };
 
+struct L3Lds {   // a staged chunk (LDS)
+    const float* p;
+    __device__ __forceinline__ double operator()(int i) const { return (double)p[i]; }
+};
+
 __global__ __launch_bounds__(256) void k_normalize(L3Args a) {
     __shared__ int16_t s_lstart[4][kL3MaxLeaves], s_llen[4][kL3MaxLeaves];
     __shared__ double s_leaf[4][kL3MaxLeaves];
     __shared__ int s_cnt[4];
+    // each 8192-sample chunk is staged with coalesced loads before the leaf sums (a
+    // lane's leaf read straight from global memory costs a scattered round trip per
+    // 8 samples)
+    __shared__ float s_x[4][8192];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int i = blockIdx.x * 4 + wave;
     if (i >= a.n) return;
@@ -155,7 +164,25 @@ __global__ __launch_bounds__(256) void k_normalize(L3Args a) {
         const int nl = s_cnt[wave];
         const L3Src xc{x.base, x.ring ? (x.start + c0) % x.ring : 0, x.ring};
         const L3Src xl = x.ring ? xc : L3Src{x.base + c0, 0, 0};
-        for (int l = lane; l < nl; l += 64) s_leaf[wave][l] = l3_leaf_sum(xl, s_lstart[wave][l], s_llen[wave][l]);
+        float* sx = s_x[wave];
+        for (int k0 = 0; k0 < cn; k0 += 64 * 8) {   // 8 loads per lane in flight
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int k = k0 + 64 * u + lane;
+                v[u] = k < cn ? (float)xl(k) : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int k = k0 + 64 * u + lane;
+                if (k < cn) sx[k] = v[u];
+            }
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        asm volatile("" ::: "memory");
+        const L3Lds xs{sx};
+        for (int l = lane; l < nl; l += 64) s_leaf[wave][l] = l3_leaf_sum(xs, s_lstart[wave][l], s_llen[wave][l]);
         asm volatile("" ::: "memory");
         __builtin_amdgcn_wave_barrier();
         double part = 0.0;
