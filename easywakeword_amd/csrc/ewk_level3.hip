@@ -8,7 +8,8 @@
 //     pairwise order (chunks of 8192, 8-accumulator leaves of <= 128, split at
 //     n2 = n/2 - (n/2)%8), every other step is elementwise IEEE arithmetic.
 //     One wave per segment, read straight from the stream ring (gathered events)
-//     or from a linear float32 batch.
+//     or from a linear float32 batch; each 8192-sample chunk is staged in LDS and its
+//     pairwise tree evaluated lane-parallel (split top-down, combined bottom-up).
 //   * k_decode_pcm16: librosa.load / soundfile / PortAudio int16 -> float32
 //     (x / 32768, exact), the WAV/PCM16 ingest of SURVEY.md 8f.2.
 #include <hip/hip_runtime.h>
@@ -21,73 +22,6 @@
 #pragma clang fp contract(off)
 
 namespace ewk {
-
-constexpr int kL3MaxLeaves = 128;   // a chunk of <= 8192 elements has <= 128 leaves
-
-// Leaves of numpy's pairwise recursion over [0, n), depth-first, left to right.
-__device__ int l3_build_leaves(int n, int16_t* lstart, int16_t* llen) {
-    int st_s[16], st_n[16];
-    int sp = 0, cnt = 0;
-    st_s[sp] = 0;
-    st_n[sp] = n;
-    ++sp;
-    while (sp > 0) {
-        --sp;
-        const int s = st_s[sp], m = st_n[sp];
-        if (m <= 128) {
-            lstart[cnt] = (int16_t)s;
-            llen[cnt] = (int16_t)m;
-            ++cnt;
-        } else {
-            int n2 = m / 2;
-            n2 -= n2 % 8;
-            st_s[sp] = s + n2; st_n[sp] = m - n2; ++sp;   // right pushed first: left visited first
-            st_s[sp] = s;      st_n[sp] = n2;     ++sp;
-        }
-    }
-    return cnt;
-}
-
-// Post-order recombination of the leaf sums: f(m) = m <= 128 ? leaf : f(n2) + f(m - n2).
-__device__ double l3_combine(int n, const double* leaf) {
-    int st_n[16], st_state[16];
-    double st_val[16];
-    int sp = 1, li = 0;
-    st_n[0] = n;
-    st_state[0] = 0;
-    double ret = 0.0;
-    while (sp > 0) {
-        const int top = sp - 1;
-        const int m = st_n[top];
-        if (m <= 128) {
-            ret = leaf[li++];
-            --sp;
-            while (sp > 0) {   // deliver ret to the parent
-                const int p = sp - 1;
-                if (st_state[p] == 1) {   // left done: keep it, descend right
-                    st_val[p] = ret;
-                    st_state[p] = 2;
-                    int n2 = st_n[p] / 2;
-                    n2 -= n2 % 8;
-                    st_n[sp] = st_n[p] - n2;
-                    st_state[sp] = 0;
-                    ++sp;
-                    break;
-                }
-                ret = st_val[p] + ret;    // right done: combine
-                --sp;
-            }
-        } else {
-            st_state[top] = 1;
-            int n2 = m / 2;
-            n2 -= n2 % 8;
-            st_n[sp] = n2;
-            st_state[sp] = 0;
-            ++sp;
-        }
-    }
-    return ret;
-}
 
 template <typename Src>
 __device__ __forceinline__ double l3_leaf_sum(const Src& x, int s, int n) {
@@ -127,16 +61,27 @@ struct L3Lds {   // a staged chunk (LDS)
     __device__ __forceinline__ double operator()(int i) const { return (double)p[i]; }
 };
 
-__global__ __launch_bounds__(256) void k_normalize(L3Args a) {
-    __shared__ int16_t s_lstart[4][kL3MaxLeaves], s_llen[4][kL3MaxLeaves];
-    __shared__ double s_leaf[4][kL3MaxLeaves];
-    __shared__ int s_cnt[4];
-    // each 8192-sample chunk is staged with coalesced loads before the leaf sums (a
-    // lane's leaf read straight from global memory costs a scattered round trip per
-    // 8 samples)
-    __shared__ float s_x[4][8192];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int i = blockIdx.x * 4 + wave;
+// numpy's pairwise recursion over one chunk, lane-parallel: the tree is split top-down
+// one depth at a time (a node of m > 128 elements splits at n2 = m/2 - (m/2)%8), each
+// leaf is summed by one lane from the staged chunk, and the internal nodes are combined
+// bottom-up as left + right -- the same additions as the recursion, so bit-identical.
+constexpr int kL3Depth = 9;     // 8192 -> <= 128 within 7 splits; uneven splits may take one more
+constexpr int kL3Nodes = 128;   // nodes per depth (a chunk has <= 128 leaves)
+
+__device__ __forceinline__ void l3_sync() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+}
+
+__global__ __launch_bounds__(64) void k_normalize(L3Args a) {
+    __shared__ float s_x[8192];                               // the staged chunk
+    __shared__ int16_t s_ns[kL3Depth][kL3Nodes], s_nl[kL3Depth][kL3Nodes], s_nc[kL3Depth][kL3Nodes];
+    __shared__ double s_nv[kL3Depth][kL3Nodes];
+    __shared__ int16_t s_leaf_d[kL3Nodes], s_leaf_k[kL3Nodes];
+    __shared__ int s_cnt[kL3Depth + 1];
+    const int lane = threadIdx.x;
+    const int i = blockIdx.x;
     if (i >= a.n) return;
     L3Src x;
     int n;
@@ -158,14 +103,9 @@ __global__ __launch_bounds__(256) void k_normalize(L3Args a) {
     double acc = 0.0;
     for (int c0 = 0; c0 < n; c0 += 8192) {
         const int cn = min(8192, n - c0);
-        if (lane == 0) s_cnt[wave] = l3_build_leaves(cn, s_lstart[wave], s_llen[wave]);
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-        const int nl = s_cnt[wave];
         const L3Src xc{x.base, x.ring ? (x.start + c0) % x.ring : 0, x.ring};
         const L3Src xl = x.ring ? xc : L3Src{x.base + c0, 0, 0};
-        float* sx = s_x[wave];
-        for (int k0 = 0; k0 < cn; k0 += 64 * 8) {   // 8 loads per lane in flight
+        for (int k0 = 0; k0 < cn; k0 += 64 * 8) {   // coalesced staging, 8 loads per lane in flight
             float v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
@@ -175,21 +115,78 @@ __global__ __launch_bounds__(256) void k_normalize(L3Args a) {
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int k = k0 + 64 * u + lane;
-                if (k < cn) sx[k] = v[u];
+                if (k < cn) s_x[k] = v[u];
             }
         }
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        asm volatile("" ::: "memory");
-        const L3Lds xs{sx};
-        for (int l = lane; l < nl; l += 64) s_leaf[wave][l] = l3_leaf_sum(xs, s_lstart[wave][l], s_llen[wave][l]);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
-        double part = 0.0;
-        if (lane == 0) part = l3_combine(cn, s_leaf[wave]);
-        acc += __shfl(part, 0, 64);
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
+        // top-down split
+        if (lane == 0) {
+            s_ns[0][0] = 0;
+            s_nl[0][0] = (int16_t)cn;
+            s_cnt[0] = 1;
+            s_cnt[kL3Depth] = 0;   // leaves
+        }
+        l3_sync();
+        int depth = 0;
+        for (int d = 0; d < kL3Depth; ++d) {
+            const int cnt = s_cnt[d];
+            int made = 0, leaves = s_cnt[kL3Depth];
+            for (int k0 = 0; k0 < cnt; k0 += 64) {
+                const int k = k0 + lane;
+                int st = 0, m = 0;
+                if (k < cnt) {
+                    st = s_ns[d][k];
+                    m = s_nl[d][k];
+                }
+                const bool split = k < cnt && m > 128;
+                const bool leaf = k < cnt && m <= 128;
+                const uint64_t ms = __ballot(split), ml = __ballot(leaf);
+                const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+                if (split) {
+                    int n2 = m / 2;
+                    n2 -= n2 % 8;
+                    const int c = 2 * (made + __popcll(ms & below));
+                    s_ns[d + 1][c] = (int16_t)st;
+                    s_nl[d + 1][c] = (int16_t)n2;
+                    s_ns[d + 1][c + 1] = (int16_t)(st + n2);
+                    s_nl[d + 1][c + 1] = (int16_t)(m - n2);
+                    s_nc[d][k] = (int16_t)c;
+                } else if (leaf) {
+                    const int q = leaves + __popcll(ml & below);
+                    s_leaf_d[q] = (int16_t)d;
+                    s_leaf_k[q] = (int16_t)k;
+                    s_nc[d][k] = -1;
+                }
+                made += __popcll(ms);
+                leaves += __popcll(ml);
+            }
+            l3_sync();
+            if (lane == 0) {   // (a chunk of <= 8192 splits at most 7 times: d + 1 < kL3Depth)
+                if (d + 1 < kL3Depth) s_cnt[d + 1] = 2 * made;
+                s_cnt[kL3Depth] = leaves;
+            }
+            l3_sync();
+            depth = d;
+            if (made == 0) break;
+        }
+        // leaf sums, one lane per leaf
+        const L3Lds xs{s_x};
+        const int nleaf = s_cnt[kL3Depth];
+        for (int q = lane; q < nleaf; q += 64) {
+            const int d = s_leaf_d[q], k = s_leaf_k[q];
+            s_nv[d][k] = l3_leaf_sum(xs, s_ns[d][k], s_nl[d][k]);
+        }
+        l3_sync();
+        // bottom-up: internal node = left + right
+        for (int d = depth - 1; d >= 0; --d) {
+            const int cnt = s_cnt[d];
+            for (int k = lane; k < cnt; k += 64) {
+                const int c = s_nc[d][k];
+                if (c >= 0) s_nv[d][k] = s_nv[d + 1][c] + s_nv[d + 1][c + 1];
+            }
+            l3_sync();
+        }
+        acc += s_nv[0][0];
+        l3_sync();
     }
     const double mean = acc / (double)n;
     // ---- np.max(np.abs(y)) (order-free)
@@ -216,7 +213,7 @@ __global__ __launch_bounds__(256) void k_normalize(L3Args a) {
 
 hipError_t launch_normalize(const L3Args& a, hipStream_t s) {
     if (a.n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_normalize, dim3((a.n + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_normalize, dim3(a.n), dim3(64), 0, s, a);   // one wave per segment
     return hipGetLastError();
 }
 
