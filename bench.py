@@ -240,7 +240,7 @@ def confirm_bench(se, ev, final_tick, batch, dev):
         return {"segments": 0}
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    audio = se.normalize_events(pos)
+    audio = se.normalize_events_device(pos)          # float64, stays on the GPU
     t1 = time.perf_counter()
     wc = WhisperConfirm(device=dev)
     wc.transcribe(audio)                            # warm-up at the timed shape (kernels, allocator)

@@ -85,8 +85,11 @@ class WhisperConfirm:
         torch = self.torch
         n = N_FRAMES * HOP
         x = torch.zeros((len(batch), n), dtype=torch.float32, device=self.device)
-        for i, a in enumerate(batch):
-            a = torch.as_tensor(np.asarray(a, np.float32)[:n], device=self.device)
+        for i, a in enumerate(batch):   # numpy arrays or device tensors (normalize_events_device)
+            if torch.is_tensor(a):
+                a = a[:n].to(device=self.device, dtype=torch.float32)
+            else:
+                a = torch.as_tensor(np.asarray(a, np.float32)[:n], device=self.device)
             x[i, :a.numel()] = a
         spec = torch.stft(x, N_FFT, HOP, window=self.window, return_complex=True)
         power = spec[..., :-1].abs() ** 2

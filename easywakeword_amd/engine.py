@@ -244,6 +244,21 @@ class StreamEngine(Engine):
         offs = np.concatenate([[0], np.cumsum(lengths)[:-1]])
         return [out[o:o + l] for o, l in zip(offs, lengths)]
 
+    def normalize_events_device(self, events: np.ndarray) -> list:
+        """normalize_events with the float64 output left in GPU memory: a list of torch
+        views on this engine's device (level 3 without the host round trip)."""
+        import torch
+        ev = np.ascontiguousarray(events, dtype=_lib.EVENT_DTYPE)
+        n = len(ev)
+        if n == 0:
+            return []
+        lengths = ev["length"].astype(np.int64)
+        out = torch.empty(max(1, int(lengths.sum())), dtype=torch.float64, device=torch.device("cuda", self.gpu))
+        check(self._lib.ewk_normalize_events(self._h, ev.ctypes.data_as(C.POINTER(_lib.EwkEvent)), n,
+                                             C.c_void_p(out.data_ptr()), _lib.EWK_OUT_DEVICE))
+        offs = np.concatenate([[0], np.cumsum(lengths)[:-1]])
+        return [out[int(o):int(o) + int(l)] for o, l in zip(offs, lengths)]
+
     def push_device(self, ptr: int, stride: int, tick_stride: int = 0, n_ticks: int = 1) -> None:
         check(self._lib.ewk_push_many(self._h, C.c_void_p(ptr), int(stride), int(tick_stride), int(n_ticks),
                                       _lib.EWK_PUSH_DEVICE))

@@ -63,9 +63,11 @@ def test_normalize_events_from_rings_bit_exact():
         ev = ev[(ev["flags"] & 1) == 0]
         if len(ev):   # normalise before the rings move on
             outs = eng.normalize_events(ev)
-            for e, y in zip(ev, outs):
+            outs_dev = eng.normalize_events_device(ev)   # the confirm stage's device-resident copy
+            for e, y, yd in zip(ev, outs, outs_dev):
                 audio = eng.read_segment(int(e["stream"]), int(e["ring_start"]), int(e["length"]))
                 np.testing.assert_array_equal(y, _numpy_normalize(audio))
+                np.testing.assert_array_equal(yd.cpu().numpy(), y)
             evs.extend(ev)
     assert len(evs) >= 6
 
