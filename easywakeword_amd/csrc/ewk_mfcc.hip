@@ -1684,12 +1684,16 @@ hipError_t launch_snapshot(const int32_t* src, int32_t* dst, hipStream_t s) {
 // histograms of the segment's pass count (64 buckets, longest first), an exclusive
 // scan, then a scatter of the indices.  The order within a bucket is arbitrary; each
 // segment's result does not depend on it.
+#ifndef EWK_LPT
+#define EWK_LPT 1   // longest-first order for large linear batches (0: index order)
+#endif
 constexpr int kLptBuckets = 64;
 constexpr int kLptWaves = 16;
 __global__ __launch_bounds__(64 * kLptWaves) void k_lpt_order(const int32_t* __restrict__ lengths, int32_t n,
-                                                               int32_t* __restrict__ order) {
+                                                               int32_t* __restrict__ order, int32_t* __restrict__ work) {
     __shared__ int hist[kLptWaves][kLptBuckets];
     const int w = threadIdx.x >> 6;
+    if (threadIdx.x == 0) *work = 0;   // the scorer's work counter (saves a fill launch)
     for (int i = threadIdx.x; i < kLptWaves * kLptBuckets; i += blockDim.x) (&hist[0][0])[i] = 0;
     __syncthreads();
     auto bucket = [](int32_t len) {
@@ -1725,19 +1729,18 @@ int score_grid(int n_seg, int ring_mode) {
 hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mode, hipStream_t s) {
     if (a.n_seg <= 0) return hipSuccess;
     const int grid = score_grid(a.n_seg, ring_mode);
-    if (!ring_mode) {   // ring mode: k_advance re-arms the counter after each tick
-        hipError_t e = hipMemsetAsync(a.work, 0, sizeof(int32_t), s);
-        if (e != hipSuccess) return e;
-    }
-    if (ring_mode) {
+    if (ring_mode) {   // ring mode: the re-score launch re-arms the counter after each tick
         hipLaunchKernelGGL(k_score_f32<1>, dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
     } else {
         ScoreArgs b = a;
         // the order only matters once the waves queue several segments each
-        if (a.order && a.n_seg > 2 * grid * WAVES)
-            hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(64 * kLptWaves), 0, s, a.lengths, a.n_seg, a.order);
-        else
+        if (EWK_LPT && a.order && a.n_seg > 2 * grid * WAVES) {
+            hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(64 * kLptWaves), 0, s, a.lengths, a.n_seg, a.order, a.work);
+        } else {
             b.order = nullptr;
+            hipError_t e = hipMemsetAsync(a.work, 0, sizeof(int32_t), s);
+            if (e != hipSuccess) return e;
+        }
         hipLaunchKernelGGL(k_score_f32<0>, dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, b);
     }
     return hipGetLastError();
