@@ -192,7 +192,7 @@ static hipError_t reserve_rescore(ewk_engine* e, int32_t n_seg) {
     err = e->rescore_buf.reserve((size_t)n_seg + 1);
     if (err != hipSuccess) return err;
     e->d_rescore = e->rescore_buf.p;
-    err = e->order.reserve((size_t)n_seg);
+    err = e->order.reserve((size_t)n_seg + kLptScratch);
     if (err != hipSuccess) return err;
     e->rescore_cap = n_seg;
     return hipSuccess;

@@ -101,6 +101,8 @@ struct ScoreArgs {
 };
 
 hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mode, hipStream_t s);
+// ScoreArgs::order holds n_seg indices followed by kLptScratch ints of bucket counters
+constexpr int kLptScratch = 128;
 // ring mode: *ev_base = *n_events after a scoring pass; zero the ring-mode work counter and re-score count
 hipError_t launch_snapshot(const int32_t* src, int32_t* dst, hipStream_t s);   // *dst = *src, stream-ordered
 hipError_t launch_advance_watermark(int32_t* ev_base, const int32_t* n_events, int32_t* work,

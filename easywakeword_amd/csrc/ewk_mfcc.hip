@@ -1680,46 +1680,59 @@ hipError_t launch_snapshot(const int32_t* src, int32_t* dst, hipStream_t s) {
 }
 
 // Longest-first work order for a linear batch (LPT: the persistent waves' last
-// segments are the shortest, so the grid drains evenly).  One workgroup: per-wave
-// histograms of the segment's pass count (64 buckets, longest first), an exclusive
-// scan, then a scatter of the indices.  The order within a bucket is arbitrary; each
-// segment's result does not depend on it.
+// segments are the shortest, so the grid drains evenly): 64 buckets of the segment's pass
+// count, longest first; the order within a bucket is arbitrary (each segment's result
+// does not depend on it).
 #ifndef EWK_LPT
 #define EWK_LPT 1   // longest-first order for large linear batches (0: index order)
 #endif
 constexpr int kLptBuckets = 64;
-constexpr int kLptWaves = 16;
-__global__ __launch_bounds__(64 * kLptWaves) void k_lpt_order(const int32_t* __restrict__ lengths, int32_t n,
-                                                               int32_t* __restrict__ order, int32_t* __restrict__ work) {
-    __shared__ int hist[kLptWaves][kLptBuckets];
-    const int w = threadIdx.x >> 6;
-    if (threadIdx.x == 0) *work = 0;   // the scorer's work counter (saves a fill launch)
-    for (int i = threadIdx.x; i < kLptWaves * kLptBuckets; i += blockDim.x) (&hist[0][0])[i] = 0;
+__device__ __forceinline__ int lpt_bucket(int32_t len) {   // longest first: bucket 0 = most passes
+    const int np = (1 + max(len, 0) / HOP + kFPP - 1) / kFPP;
+    return kLptBuckets - 1 - min(np, kLptBuckets - 1);
+}
+
+// Grid-parallel LPT order: pass 1 adds each workgroup's bucket histogram of its slice to
+// the global totals; pass 2 (every workgroup redoes the 64-bucket exclusive scan) reserves a
+// contiguous run per bucket with one atomic on that bucket's cursor and scatters its
+// indices.  cnt = order + n: [0, 64) totals, [64, 128) cursors (zeroed before pass 1).
+constexpr int kLptBlock = 256;
+__global__ __launch_bounds__(kLptBlock) void k_lpt_hist(const int32_t* __restrict__ lengths, int32_t n,
+                                                        int32_t* __restrict__ cnt) {
+    __shared__ int h[kLptBuckets];
+    if (threadIdx.x < kLptBuckets) h[threadIdx.x] = 0;
     __syncthreads();
-    auto bucket = [](int32_t len) {
-        const int np = (1 + max(len, 0) / HOP + kFPP - 1) / kFPP;
-        return kLptBuckets - 1 - min(np, kLptBuckets - 1);
-    };
-    for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&hist[w][bucket(lengths[i])], 1);
+    for (int i = blockIdx.x * kLptBlock + threadIdx.x; i < n; i += gridDim.x * kLptBlock)
+        atomicAdd(&h[lpt_bucket(lengths[i])], 1);
     __syncthreads();
-    if (threadIdx.x < kLptBuckets) {   // bucket-major, wave-minor exclusive scan (one wave, lane = bucket)
-        const int b = threadIdx.x;
-        int tot = 0;
-        for (int ww = 0; ww < kLptWaves; ++ww) tot += hist[ww][b];
+    if (threadIdx.x < kLptBuckets && h[threadIdx.x]) atomicAdd(&cnt[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(kLptBlock) void k_lpt_scatter(const int32_t* __restrict__ lengths, int32_t n,
+                                                           int32_t* __restrict__ order, int32_t* __restrict__ cnt,
+                                                           int32_t* __restrict__ work) {
+    __shared__ int h[kLptBuckets], base[kLptBuckets];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *work = 0;   // the scorer's work counter (no fill launch)
+    if (threadIdx.x < kLptBuckets) h[threadIdx.x] = 0;
+    __syncthreads();
+    for (int i = blockIdx.x * kLptBlock + threadIdx.x; i < n; i += gridDim.x * kLptBlock)
+        atomicAdd(&h[lpt_bucket(lengths[i])], 1);
+    __syncthreads();
+    if (threadIdx.x < kLptBuckets) {   // one wave: lane = bucket
+        const int b = threadIdx.x, tot = cnt[b];
         int incl = tot;
         for (int d = 1; d < kLptBuckets; d <<= 1) {
             const int t = __shfl_up(incl, d, 64);
             if (b >= d) incl += t;
         }
-        int run = incl - tot;
-        for (int ww = 0; ww < kLptWaves; ++ww) {
-            const int c = hist[ww][b];
-            hist[ww][b] = run;
-            run += c;
-        }
+        base[b] = (incl - tot) + (h[b] ? atomicAdd(&cnt[kLptBuckets + b], h[b]) : 0);
+        h[b] = 0;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) order[atomicAdd(&hist[w][bucket(lengths[i])], 1)] = i;
+    for (int i = blockIdx.x * kLptBlock + threadIdx.x; i < n; i += gridDim.x * kLptBlock) {
+        const int b = lpt_bucket(lengths[i]);
+        order[base[b] + atomicAdd(&h[b], 1)] = i;
+    }
 }
 
 int score_grid(int n_seg, int ring_mode) {
@@ -1735,7 +1748,12 @@ hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mo
         ScoreArgs b = a;
         // the order only matters once the waves queue several segments each
         if (EWK_LPT && a.order && a.n_seg > 2 * grid * WAVES) {
-            hipLaunchKernelGGL(k_lpt_order, dim3(1), dim3(64 * kLptWaves), 0, s, a.lengths, a.n_seg, a.order, a.work);
+            int32_t* cnt = a.order + a.n_seg;
+            hipError_t e = hipMemsetAsync(cnt, 0, 2 * kLptBuckets * sizeof(int32_t), s);
+            if (e != hipSuccess) return e;
+            const int g = std::min(256, (a.n_seg + kLptBlock - 1) / kLptBlock);
+            hipLaunchKernelGGL(k_lpt_hist, dim3(g), dim3(kLptBlock), 0, s, a.lengths, a.n_seg, cnt);
+            hipLaunchKernelGGL(k_lpt_scatter, dim3(g), dim3(kLptBlock), 0, s, a.lengths, a.n_seg, a.order, cnt, a.work);
         } else {
             b.order = nullptr;
             hipError_t e = hipMemsetAsync(a.work, 0, sizeof(int32_t), s);
