@@ -494,8 +494,7 @@ static int score_linear(ewk_engine* e, const float* d_pcm, const int64_t* d_off,
     a.out_score = d_score;
     a.out_match = d_match;
     if (!a.has_template) a.rescore_list = nullptr;
-    HIP_TRY(hipMemsetAsync(e->d_rescore, 0, sizeof(int32_t), s));
-    {
+    {   // (launch_score_f32 zeroes the work counter and the re-score count)
         ProfScope ps(e, 0, s);
         HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));
     }
@@ -583,8 +582,7 @@ int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int
         a.out_match = e->match.p;
         a.cand_f32 = (flags & EWK_SCORE_F32_CANDIDATES) ? 1 : 0;
         if (!a.has_template) a.rescore_list = nullptr;
-        HIP_TRY(hipMemsetAsync(e->d_rescore, 0, sizeof(int32_t), s));
-        HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));
+        HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));   // (zeroes the work counter and the re-score count)
         if (a.has_template) {
             const int64_t tmax = std::max<int64_t>(1 + e->ring_len / HOP, 1 + max_len / HOP);
             HIP_TRY(launch_score_f64(e->d_tab64, a, 0, e->f64_scratch.p, tmax * (NMEL + NMFCC), e->f64_grid,

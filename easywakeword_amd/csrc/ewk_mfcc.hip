@@ -1710,9 +1710,12 @@ __global__ __launch_bounds__(kLptBlock) void k_lpt_hist(const int32_t* __restric
 
 __global__ __launch_bounds__(kLptBlock) void k_lpt_scatter(const int32_t* __restrict__ lengths, int32_t n,
                                                            int32_t* __restrict__ order, int32_t* __restrict__ cnt,
-                                                           int32_t* __restrict__ work) {
+                                                           int32_t* __restrict__ work, int32_t* __restrict__ rescore_count) {
     __shared__ int h[kLptBuckets], base[kLptBuckets];
-    if (blockIdx.x == 0 && threadIdx.x == 0) *work = 0;   // the scorer's work counter (no fill launch)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {   // the scorer's counters (no fill launches)
+        *work = 0;
+        if (rescore_count) *rescore_count = 0;
+    }
     if (threadIdx.x < kLptBuckets) h[threadIdx.x] = 0;
     __syncthreads();
     for (int i = blockIdx.x * kLptBlock + threadIdx.x; i < n; i += gridDim.x * kLptBlock)
@@ -1753,10 +1756,12 @@ hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mo
             if (e != hipSuccess) return e;
             const int g = std::min(256, (a.n_seg + kLptBlock - 1) / kLptBlock);
             hipLaunchKernelGGL(k_lpt_hist, dim3(g), dim3(kLptBlock), 0, s, a.lengths, a.n_seg, cnt);
-            hipLaunchKernelGGL(k_lpt_scatter, dim3(g), dim3(kLptBlock), 0, s, a.lengths, a.n_seg, a.order, cnt, a.work);
+            hipLaunchKernelGGL(k_lpt_scatter, dim3(g), dim3(kLptBlock), 0, s, a.lengths, a.n_seg, a.order, cnt, a.work,
+                               a.rescore_count);
         } else {
             b.order = nullptr;
             hipError_t e = hipMemsetAsync(a.work, 0, sizeof(int32_t), s);
+            if (e == hipSuccess && a.rescore_count) e = hipMemsetAsync(a.rescore_count, 0, sizeof(int32_t), s);
             if (e != hipSuccess) return e;
         }
         hipLaunchKernelGGL(k_score_f32<0>, dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, b);
