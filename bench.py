@@ -382,6 +382,7 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
            "kernel_times": f"separate instrumented pass of {prof_ticks} ticks",
            "events": int(len(real)), "matches": int(real["match"].sum()) if len(real) else 0,
            "mfcc_frames": int((1 + real["length"].astype(np.int64) // HOP).sum()) if len(real) else 0}
+    out["mfcc_frames_per_s"] = out["mfcc_frames"] / wall   # gated segments scored, over the timed ticks
     if world > 1:
         out["positives_gathered_to_rank0"] = gathered[0]
     if confirm_batch > 0:   # config 5: level 3 on the latest positives still in the rings
