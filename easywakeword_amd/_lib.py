@@ -47,7 +47,7 @@ EXPORTS = [
 class EwkConfig(C.Structure):
     _fields_ = [
         ("sample_rate", C.c_int32), ("buffer_seconds", C.c_int32), ("block", C.c_int32),
-        ("reserved0", C.c_int32), ("tick_seconds", C.c_double), ("pre_speech_silence", C.c_double),
+        ("ring_samples", C.c_int32), ("tick_seconds", C.c_double), ("pre_speech_silence", C.c_double),
         ("speech_duration_min", C.c_double), ("speech_duration_max", C.c_double),
         ("post_speech_silence", C.c_double), ("padding", C.c_double), ("max_segment_seconds", C.c_double),
         ("similarity_threshold", C.c_double), ("reentry_timeout", C.c_double), ("min_threshold", C.c_double),

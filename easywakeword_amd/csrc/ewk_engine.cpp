@@ -66,7 +66,8 @@ struct ewk_engine {
     hipStream_t stream = nullptr;
     ewk_config cfg{};
     int32_t n_streams = 0;
-    int64_t ring_len = 0;
+    int64_t ring_len = 0;           // the reference ring (buffer_seconds * sample_rate)
+    int64_t sring_len = 0;          // samples stored per stream (ring_len, or cfg.ring_samples)
     int32_t n_blocks = 0;
     int64_t n_last = 0;
 
@@ -302,6 +303,27 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
         return fail(EWK_EINVAL, "speech_duration_min must be <= speech_duration_max");
     if (c.post_speech_silence <= 0) return fail(EWK_EINVAL, "post_speech_silence must be positive");
     if (n_streams < 0) return fail(EWK_EINVAL, "n_streams must be >= 0");
+    const int64_t ring_len = (int64_t)c.buffer_seconds * c.sample_rate;
+    if (ring_len > INT32_MAX / 2) return fail(EWK_EINVAL, "buffer_seconds too large");
+    // Longest segment request the cut can make (wakeword.py:1100-1111): nreq =
+    // int(|sound_start - now - padding| * sr) with now - sound_start <= max speech +
+    // (post silence rounded up to a tick), capped at the ring (return_last_n_seconds).
+    const int64_t seg_need = std::min<int64_t>(
+        ring_len, (int64_t)((c.speech_duration_max + c.post_speech_silence + c.tick_seconds + c.padding) *
+                            (double)c.sample_rate) + 2);
+    if (c.ring_samples != 0) {
+        if (c.ring_samples < 0 || c.ring_samples > ring_len)
+            return fail(EWK_EINVAL, "ring_samples must be in [0, buffer_seconds * sample_rate]");
+        if (c.ring_samples < ring_len) {
+            if (ring_len % c.block != 0 || c.ring_samples % c.block != 0)
+                return fail(EWK_EINVAL, "a compact ring (ring_samples) needs block to divide both rings");
+            if (gate_stage_len(c.block, (int64_t)(0.1 * (double)c.sample_rate)) < c.block)
+                return fail(EWK_EINVAL, "a compact ring (ring_samples) needs block <= 4096");
+            if (c.ring_samples < seg_need + c.block || c.ring_samples < (int64_t)(0.1 * (double)c.sample_rate))
+                return fail(EWK_EINVAL, "ring_samples must hold the longest segment request plus one tick (" +
+                                            std::to_string(seg_need + c.block) + " samples for this config)");
+        }
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(EWK_ENODEV, "no HIP device visible");
     if (device < 0 || device >= ndev) return fail(EWK_ENODEV, "device index out of range");
@@ -311,7 +333,8 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
     e->device = device;
     e->cfg = c;
     e->n_streams = n_streams;
-    e->ring_len = (int64_t)c.buffer_seconds * c.sample_rate;
+    e->ring_len = ring_len;
+    e->sring_len = c.ring_samples > 0 ? (int64_t)c.ring_samples : ring_len;
     e->n_blocks = (int32_t)(e->ring_len / c.block);
     e->n_last = (int64_t)(0.1 * (double)c.sample_rate);   // int(0.1 * FREQUENCY)
     auto bail = [&](hipError_t err, const char* what) {
@@ -355,12 +378,12 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
     if ((err = hipMemset(e->d_work, 0, 8 * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
     // fp64 scratch: log-mel + mfcc rows for the longest ring segment
     {
-        const int64_t tmax = 1 + e->ring_len / HOP;
+        const int64_t tmax = 1 + e->sring_len / HOP;
         const int64_t per = tmax * (NMEL + NMFCC);
         if ((err = e->f64_scratch.reserve((size_t)per * e->f64_grid)) != hipSuccess) return bail(err, "f64 scratch");
     }
     if (n_streams > 0) {
-        const size_t ring_bytes = (size_t)n_streams * e->ring_len * sizeof(float);
+        const size_t ring_bytes = (size_t)n_streams * e->sring_len * sizeof(float);
         if ((err = hipMalloc(&e->d_ring, ring_bytes)) != hipSuccess) return bail(err, "ring");
         if ((err = hipMalloc(&e->d_brms, (size_t)n_streams * std::max(1, e->n_blocks) * sizeof(double))) != hipSuccess)
             return bail(err, "block rms");
@@ -389,18 +412,19 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
             return bail(err, "events");
         if ((err = hipMalloc(&e->d_evc, 8 * sizeof(int32_t))) != hipSuccess) return bail(err, "event counters");
         e->gate_stage = gate_stage_len(c.block, e->n_last);
-        {   // overlap scoring with the next gate only if the next launch cannot reach a
-            // scorable segment: 2 launches of ticks + the longest segment and its trailing
-            // silence must fit in the ring
-            const double sr = (double)c.sample_rate;
-            const int64_t seg_max = (int64_t)(c.max_segment_seconds * sr) +
-                                    (int64_t)((c.post_speech_silence + c.padding + 2.0 * c.tick_seconds) * sr) + c.block;
-            const int64_t tpl = std::min<int64_t>(32, (e->ring_len - seg_max) / (2 * (int64_t)c.block));
+        {   // A segment is cut at the tick that ends it and scored after its gate launch,
+            // so the ticks of one launch after the cut must not reach its first sample:
+            // ticks_per_launch <= (ring - longest request) / block (>= 1: a one-tick launch is
+            // always safe, the cut never asks for more than the ring).  Overlapping the
+            // scoring with the next gate launch doubles the ticks that may pass.
+            const int64_t room = (e->sring_len - std::min(seg_need, e->sring_len)) / (int64_t)c.block;
+            const int64_t tpl = std::max<int64_t>(1, std::min<int64_t>(32, room));
+            const int64_t tpl_ov = std::min<int64_t>(32, room / 2);
             // opt-in (EWK_SCORE_OVERLAP=1): measured on MI355X the extra stream/event calls
             // per tick cost more host time than the concurrency saves (scripts/mb_stream.py)
             const char* env = getenv("EWK_SCORE_OVERLAP");
-            e->overlap = tpl >= 1 && env && env[0] == '1';
-            e->ticks_per_launch = e->overlap ? (int32_t)tpl : 32;
+            e->overlap = tpl_ov >= 1 && env && env[0] == '1';
+            e->ticks_per_launch = (int32_t)(e->overlap ? tpl_ov : tpl);
         }
         int rc = ewk_reset_streams(e);
         if (rc != EWK_OK) {
@@ -664,7 +688,7 @@ int ewk_reset_streams(ewk_engine* e) {
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = e->stream;
     HIP_TRY(join_scoring(e, s));
-    HIP_TRY(hipMemsetAsync(e->d_ring, 0, (size_t)e->n_streams * e->ring_len * sizeof(float), s));
+    HIP_TRY(hipMemsetAsync(e->d_ring, 0, (size_t)e->n_streams * e->sring_len * sizeof(float), s));
     HIP_TRY(hipMemsetAsync(e->d_brms, 0, (size_t)e->n_streams * std::max(1, e->n_blocks) * sizeof(double), s));
     std::vector<GateStream> st(e->n_streams);
     for (auto& x : st) {
@@ -687,7 +711,7 @@ static int score_pending(ewk_engine* e, hipStream_t ss, const int32_t* n_events)
     if (!e->has_tmpl) return EWK_OK;   // events keep NaN scores until a template exists
     ScoreArgs a = base_args(e);
     a.pcm = e->d_ring;
-    a.ring_len = e->ring_len;
+    a.ring_len = e->sring_len;
     a.events = e->ev_bank(e->bank);
     a.n_events = n_events;
     a.ev_base = e->evc_bank(e->bank) + 2;
@@ -698,7 +722,7 @@ static int score_pending(ewk_engine* e, hipStream_t ss, const int32_t* n_events)
         ProfScope ps(e, 0, ss);
         HIP_TRY(launch_score_f32(e->d_tab, a, 1, ss));
     }
-    const int64_t per = (1 + e->ring_len / HOP) * (NMEL + NMFCC);
+    const int64_t per = (1 + e->sring_len / HOP) * (NMEL + NMFCC);
     {
         ProfScope ps(e, 1, ss);
         // the re-score launch also advances the watermark (its last workgroup: k_advance folded in)
@@ -763,6 +787,8 @@ static int push_impl(ewk_engine* e, const void* pcm_any, int64_t stride, int64_t
         g.tick0 = e->tick;
         g.ring = e->d_ring;
         g.ring_len = e->ring_len;
+        g.sring_len = e->sring_len;
+        g.compact = e->sring_len < e->ring_len ? 1 : 0;
         g.block_rms = e->d_brms;
         g.sorted_rms = e->d_sorted;
         g.trees = e->d_trees;
@@ -862,7 +888,7 @@ static int normalize_impl(ewk_engine* e, const float* d_pcm, const int64_t* offs
         HIP_TRY(hipMemcpyAsync(d_ev.p, events, n * sizeof(ewk_event), hipMemcpyHostToDevice, s));
         a.events = d_ev.p;
         a.pcm = e->d_ring;
-        a.ring_len = e->ring_len;
+        a.ring_len = e->sring_len;
     } else {
         HIP_TRY(d_off.reserve(std::max<int32_t>(1, n)));
         HIP_TRY(d_len.reserve(std::max<int32_t>(1, n)));
@@ -913,7 +939,7 @@ int ewk_normalize_events(ewk_engine* e, const ewk_event* events, int32_t n, doub
     if (e->n_streams <= 0) return fail(EWK_EINVAL, "engine has no streams");
     for (int32_t i = 0; i < n; ++i)
         if (events[i].stream < 0 || events[i].stream >= e->n_streams || events[i].length < 0 ||
-            events[i].length > e->ring_len || events[i].ring_start < 0 || events[i].ring_start >= e->ring_len)
+            events[i].length > e->sring_len || events[i].ring_start < 0 || events[i].ring_start >= e->sring_len)
             return fail(EWK_EINVAL, "event " + std::to_string(i) + " outside the rings");
     HIP_TRY(hipSetDevice(e->device));
     return normalize_impl(e, nullptr, nullptr, nullptr, events, n, out, flags);
@@ -941,37 +967,69 @@ int ewk_decode_pcm16(ewk_engine* e, const int16_t* in, int64_t n, float* out, in
     return EWK_OK;
 }
 
-// Copy out one bank's events once the pushes into it have completed (copy stream,
-// no wait on later work), then re-arm its counters on the engine stream.
-static int drain_bank(ewk_engine* e, int b, ewk_event* out, int32_t cap, int32_t* n_out) {
-    *n_out = 0;
+// Event banks are drained in two steps so a failing poll consumes nothing:
+// peek_bank waits for the pushes into bank b (copy stream only, no wait on later
+// work) and fetches its counters with the first kPollChunk events; take_bank copies
+// the rest out and re-arms the bank's counters on the engine stream.
+constexpr size_t kPollRegion = 16 + (size_t)kPollChunk * sizeof(ewk_event);
+
+struct BankPeek {
+    int32_t n = 0;         // queued events (<= ev_cap)
+    int32_t dropped = 0;   // events lost to a full bank
+    bool used = false;
+};
+
+static int peek_bank(ewk_engine* e, int b, BankPeek* pk) {
+    *pk = BankPeek();
     if (!e->bank_used[b]) return EWK_OK;
-    if (!e->h_poll)
-        HIP_TRY(hipHostMalloc((void**)&e->h_poll, 16 + (size_t)kPollChunk * sizeof(ewk_event), hipHostMallocDefault));
-    int32_t* cnt = reinterpret_cast<int32_t*>(e->h_poll);
-    ewk_event* spec = reinterpret_cast<ewk_event*>(e->h_poll + 16);
+    if (!e->h_poll) HIP_TRY(hipHostMalloc((void**)&e->h_poll, 2 * kPollRegion, hipHostMallocDefault));
+    unsigned char* reg = e->h_poll + b * kPollRegion;
+    int32_t* cnt = reinterpret_cast<int32_t*>(reg);
     const int32_t chunk = std::min<int32_t>(kPollChunk, e->ev_cap);
     HIP_TRY(hipStreamWaitEvent(e->cstream, e->bank_done[b], 0));
     HIP_TRY(hipMemcpyAsync(cnt, e->evc_bank(b), 4 * sizeof(int32_t), hipMemcpyDeviceToHost, e->cstream));
-    HIP_TRY(hipMemcpyAsync(spec, e->ev_bank(b), (size_t)chunk * sizeof(ewk_event), hipMemcpyDeviceToHost,
+    HIP_TRY(hipMemcpyAsync(reg + 16, e->ev_bank(b), (size_t)chunk * sizeof(ewk_event), hipMemcpyDeviceToHost,
                            e->cstream));
     HIP_TRY(hipStreamSynchronize(e->cstream));
-    int32_t n = std::min(cnt[0], e->ev_cap);
-    if (cnt[1] > 0) return fail(EWK_ENOMEM, "event queue overflow: " + std::to_string(cnt[1]) + " events dropped");
-    if (n > std::max(0, cap)) return fail(EWK_EINVAL, "poll capacity smaller than the queued events");
-    if (n > 0 && out) {
-        memcpy(out, spec, (size_t)std::min(n, chunk) * sizeof(ewk_event));
-        if (n > chunk) {
-            HIP_TRY(hipMemcpyAsync(out + chunk, e->ev_bank(b) + chunk, (size_t)(n - chunk) * sizeof(ewk_event),
+    pk->n = std::min(cnt[0], e->ev_cap);
+    pk->dropped = cnt[1];
+    pk->used = true;
+    return EWK_OK;
+}
+
+// Re-arm bank b (stream-ordered before any later push into it).
+static int rearm_bank(ewk_engine* e, int b) {
+    HIP_TRY(hipMemsetAsync(e->evc_bank(b), 0, 4 * sizeof(int32_t), e->stream));
+    e->bank_used[b] = false;
+    return EWK_OK;
+}
+
+static int take_bank(ewk_engine* e, int b, const BankPeek& pk, ewk_event* out) {
+    if (!pk.used) return EWK_OK;
+    const int32_t chunk = std::min<int32_t>(kPollChunk, e->ev_cap);
+    if (pk.n > 0 && out) {
+        memcpy(out, e->h_poll + b * kPollRegion + 16, (size_t)std::min(pk.n, chunk) * sizeof(ewk_event));
+        if (pk.n > chunk) {
+            HIP_TRY(hipMemcpyAsync(out + chunk, e->ev_bank(b) + chunk, (size_t)(pk.n - chunk) * sizeof(ewk_event),
                                    hipMemcpyDeviceToHost, e->cstream));
             HIP_TRY(hipStreamSynchronize(e->cstream));
         }
     }
-    // re-arm: stream-ordered before any later push into this bank
-    HIP_TRY(hipMemsetAsync(e->evc_bank(b), 0, 4 * sizeof(int32_t), e->stream));
-    e->bank_used[b] = false;
-    *n_out = n;
-    return EWK_OK;
+    return rearm_bank(e, b);
+}
+
+// An overflowed bank cannot be delivered whole: re-arm it (its events are lost, the
+// engine keeps running) and report how many were dropped.
+static int overflow(ewk_engine* e, const BankPeek* pk, const int* banks, int nb) {
+    int64_t lost = 0;
+    for (int i = 0; i < nb; ++i)
+        if (pk[i].used && pk[i].dropped > 0) {
+            lost += (int64_t)pk[i].n + pk[i].dropped;
+            int rc = rearm_bank(e, banks[i]);
+            if (rc) return rc;
+        }
+    return fail(EWK_ENOMEM, "event queue overflow: " + std::to_string(lost) +
+                                " events of the overflowed bank(s) dropped; the queue was re-armed");
 }
 
 static void sort_events(ewk_event* out, int32_t n) {   // deterministic order: (tick, stream)
@@ -980,20 +1038,39 @@ static void sort_events(ewk_event* out, int32_t n) {   // deterministic order: (
     });
 }
 
+static int poll_banks(ewk_engine* e, const int* banks, int nb, ewk_event* out, int32_t cap, int32_t* n_out) {
+    BankPeek pk[2];
+    int64_t total = 0;
+    bool over = false;
+    for (int i = 0; i < nb; ++i) {
+        int rc = peek_bank(e, banks[i], &pk[i]);
+        if (rc) return rc;
+        total += pk[i].n;
+        over = over || pk[i].dropped > 0;
+    }
+    if (over) return overflow(e, pk, banks, nb);
+    // validated before either bank is consumed: a short `cap` loses nothing
+    if (out && total > std::max(0, cap))
+        return fail(EWK_EINVAL, "poll capacity " + std::to_string(cap) + " is smaller than the " +
+                                    std::to_string(total) + " queued events (nothing was drained)");
+    int32_t n = 0;
+    for (int i = 0; i < nb; ++i) {
+        int rc = take_bank(e, banks[i], pk[i], out ? out + n : nullptr);
+        if (rc) return rc;
+        n += pk[i].n;
+    }
+    if (out) sort_events(out, n);
+    *n_out = n;
+    return EWK_OK;
+}
+
 int ewk_poll(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out) {
     if (!e || !n_out) return fail(EWK_EINVAL, "NULL argument");
     *n_out = 0;
     if (e->n_streams <= 0) return EWK_OK;
     HIP_TRY(hipSetDevice(e->device));
-    int32_t n0 = 0, n1 = 0;
-    const int older = e->bank ^ 1;
-    int rc = drain_bank(e, older, out, cap, &n0);
-    if (rc) return rc;
-    rc = drain_bank(e, e->bank, out ? out + n0 : nullptr, cap - n0, &n1);
-    if (rc) return rc;
-    if (out) sort_events(out, n0 + n1);
-    *n_out = n0 + n1;
-    return EWK_OK;
+    const int banks[2] = {e->bank ^ 1, e->bank};   // older first
+    return poll_banks(e, banks, 2, out, cap, n_out);
 }
 
 int ewk_poll_lagged(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out) {
@@ -1002,11 +1079,11 @@ int ewk_poll_lagged(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out) 
     if (e->n_streams <= 0) return EWK_OK;
     HIP_TRY(hipSetDevice(e->device));
     const int older = e->bank ^ 1;
-    int rc = drain_bank(e, older, out, cap, n_out);
-    if (rc) return rc;
-    if (out) sort_events(out, *n_out);
-    e->bank = older;   // later pushes append to the drained bank; the newest one drains next time
-    return EWK_OK;
+    const int banks[1] = {older};
+    int rc = poll_banks(e, banks, 1, out, cap, n_out);
+    if (rc == EWK_OK || !e->bank_used[older])   // drained (or re-armed after an overflow)
+        e->bank = older;   // later pushes append to the drained bank; the newest one drains next time
+    return rc;
 }
 
 int ewk_get_stream_state(ewk_engine* e, int32_t stream, ewk_stream_state* out) {
@@ -1034,11 +1111,11 @@ int ewk_get_stream_state(ewk_engine* e, int32_t stream, ewk_stream_state* out) {
 int ewk_read_segment(ewk_engine* e, int32_t stream, int64_t ring_start, int32_t length, float* out) {
     if (!e || !out) return fail(EWK_EINVAL, "NULL argument");
     if (stream < 0 || stream >= e->n_streams) return fail(EWK_EINVAL, "stream index out of range");
-    if (length < 0 || length > e->ring_len || ring_start < 0 || ring_start >= e->ring_len)
+    if (length < 0 || length > e->sring_len || ring_start < 0 || ring_start >= e->sring_len)
         return fail(EWK_EINVAL, "segment out of range");
     HIP_TRY(hipSetDevice(e->device));
-    const float* base = e->d_ring + (size_t)stream * e->ring_len;
-    const int64_t first = std::min<int64_t>(length, e->ring_len - ring_start);
+    const float* base = e->d_ring + (size_t)stream * e->sring_len;
+    const int64_t first = std::min<int64_t>(length, e->sring_len - ring_start);
     HIP_TRY(hipMemcpyAsync(out, base + ring_start, first * sizeof(float), hipMemcpyDeviceToHost, e->stream));
     if (length > first)
         HIP_TRY(hipMemcpyAsync(out + first, base, (length - first) * sizeof(float), hipMemcpyDeviceToHost, e->stream));
@@ -1049,14 +1126,19 @@ int ewk_read_segment(ewk_engine* e, int32_t stream, int64_t ring_start, int32_t 
 int ewk_read_last(ewk_engine* e, int32_t stream, int64_t n_samples, float* out, int64_t* n_out) {
     if (!e || !out || !n_out) return fail(EWK_EINVAL, "NULL argument");
     if (stream < 0 || stream >= e->n_streams) return fail(EWK_EINVAL, "stream index out of range");
-    ewk_stream_state st;
-    int rc = ewk_get_stream_state(e, stream, &st);
-    if (rc) return rc;
+    // return_last_n_seconds: at most the reference ring (wakeword.py:500-502)
     int64_t n = std::min<int64_t>(std::max<int64_t>(n_samples, 0), e->ring_len);
+    *n_out = 0;
+    if (n > e->sring_len)
+        return fail(EWK_EINVAL, "the compact ring keeps only the last " + std::to_string(e->sring_len) + " samples");
+    HIP_TRY(hipSetDevice(e->device));
+    GateStream st;
+    HIP_TRY(hipMemcpyAsync(&st, e->d_st + stream, sizeof(st), hipMemcpyDeviceToHost, e->stream));
+    HIP_TRY(hipStreamSynchronize(e->stream));
     *n_out = n;
     if (n == 0) return EWK_OK;
-    int64_t start = st.pointer - n;
-    if (start < 0) start += e->ring_len;
+    int64_t start = st.spos - n;
+    if (start < 0) start += e->sring_len;
     return ewk_read_segment(e, stream, start, (int32_t)n, out);
 }
 

@@ -28,7 +28,7 @@ struct GateStream {
     int32_t filled;          // block RMS cache + sorted copy valid
     int32_t reentries;
     int32_t sorted_sel;      // which of the two sorted_rms halves is current
-    int32_t pad;
+    int32_t spos;            // write position in the sample ring (== pointer when it is the full ring)
 };
 
 // numpy's pairwise summation order (np.add.reduce on a contiguous float64 array,
@@ -64,8 +64,11 @@ struct GateArgs {
     int32_t n_ticks;
     int32_t n_streams;
     int64_t tick0;           // ticks already delivered
-    float* ring;             // [n_streams][ring_len]
-    int64_t ring_len;
+    float* ring;             // [n_streams][sring_len] sample rings
+    int64_t ring_len;        // the reference ring (buffer_seconds * sample_rate): blocks, pointer, fill
+    int64_t sring_len;       // samples stored per stream (== ring_len, or a compact ring: see ewk_config.ring_samples)
+    int32_t compact;         // sring_len < ring_len (block-aligned; block RMSs kept from the first write)
+    int32_t pad0;
     double* block_rms;       // [n_streams][n_blocks] RMS of each physical block
     double* sorted_rms;      // [n_streams][2][n_blocks] the same values, ascending (double-buffered)
     GateStream* st;

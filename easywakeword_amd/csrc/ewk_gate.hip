@@ -405,7 +405,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
     double* val = reinterpret_cast<double*>(w);
     float* stage = reinterpret_cast<float*>(w + (size_t)g.val_len * 8);
 
-    const int R = (int)g.ring_len;
+    const int R = (int)g.ring_len;        // the reference ring: block grid, pointer, fill level
+    const int Rs = (int)g.sring_len;      // samples stored per stream (== R unless compact)
     const int fs = g.block;
     const int nb = g.n_blocks;
     const int nl = (int)min<int64_t>(g.n_last, g.ring_len);
@@ -448,7 +449,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
     if (dma) dma_tick(s, 0);
     else load_chunk(0, 0);
     for (;;) {
-    float* ring = g.ring + (int64_t)s * R;
+    float* ring = g.ring + (int64_t)s * Rs;
     GateStream st = g.st[s];
     double* grms = g.block_rms + (int64_t)s * nb;
     double* sorted2 = g.sorted_rms + (int64_t)s * 2 * nb;
@@ -486,6 +487,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
         }
         // ---- a1: ingest `fs` samples at the write pointer (and stage them in LDS)
         const int p0 = st.pointer;
+        const int sp0 = st.spos;    // == p0 for the full ring
         // chunks of kIngestLoads loads per lane in flight before any store (the ring may
         // alias the input as far as the compiler knows: a load-store loop serialises them);
         // chunk 0 of this tick was requested before the previous tick's compute
@@ -504,8 +506,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
                 for (int c = 0; c < 4; ++c) {
                     const int i = 256 * (h + c) + 4 * lane;
                     if (i < fs && !(EWK_GATE_ABLATE & 2)) {
-                        int k = p0 + i;
-                        if (k >= R) k -= R;
+                        int k = sp0 + i;
+                        if (k >= Rs) k -= Rs;
                         *reinterpret_cast<float4*>(ring + k) = xv[c];
                     }
                 }
@@ -524,8 +526,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
                 for (int m = 0; m < kIngestLoads; ++m) {
                     const int i = c0 + lane + 64 * m;
                     if (i < fs) {
-                        int k = p0 + i;
-                        if (k >= R) k -= R;
+                        int k = sp0 + i;
+                        if (k >= Rs) k -= Rs;
                         ring[k] = xin[m];
                     }
                 }
@@ -537,8 +539,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
             for (int m = 0; m < kIngestLoads; ++m) {
                 const int i = c0 + lane + 64 * m;
                 if (i < fs) {
-                    int k = p0 + i;
-                    if (k >= R) k -= R;
+                    int k = sp0 + i;
+                    if (k >= Rs) k -= Rs;
 #if EWK_GATE_NT & 2
                     __builtin_nontemporal_store(xin[m], ring + k);
 #else
@@ -553,6 +555,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
         wave_sync();
         const bool wrapped = p0 + fs > R;
         st.pointer = (int32_t)((p0 + fs) % R);
+        st.spos = (int32_t)((sp0 + fs) % Rs);
         st.collected = min(st.collected + (int64_t)fs, (int64_t)R);
         const bool full = st.collected >= R;
         GT_TS(q1);
@@ -566,9 +569,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
                 const int a0 = b * fs;
                 if (staged && a0 == p0)   // the block is exactly this tick's samples
                     return pw_sumsq([&](int c0) { return LdsSrc{stage + c0}; }, fs, tbf, tbr, lane, val);
-                return pw_sumsq([&](int c0) { return RingSrc{ring, a0 + c0, R}; }, fs, tbf, tbr, lane, val);
+                // reference-ring position a0 + c0 lives at sample-ring position sp0 + (a0 + c0 - p0)
+                // (the identity for the full ring; compact rings only reach this path for
+                // blocks written within the last Rs samples)
+                return pw_sumsq([&](int c0) {
+                    int k = (sp0 + (a0 + c0 - p0)) % Rs;
+                    if (k < 0) k += Rs;
+                    return RingSrc{ring, k, Rs};
+                }, fs, tbf, tbr, lane, val);
             };
-            if (!st.filled) {
+            if (!st.filled && g.compact) {
+                // compact ring: every block RMS was kept as its samples arrived (the blocks
+                // are whole ticks); the last one is this tick's, then the first sort
+                const int b = p0 / fs;
+                const double v = sqrt(block_sum(b) / (double)fs);
+                if (RB > 0) reg_set(gr, b, v, lane);
+                else if (lane == 0) grms[b] = v;
+                __threadfence_block();
+                wave_sync();
+                if (RB > 0) reg_rank_sort(gr, srt, nb, val, lane);
+                else rank_sort(grms, sorted2, nb, lane);
+                st.sorted_sel = 0;
+                st.filled = 1;
+            } else if (!st.filled) {
                 for (int b = 0; b < nb; ++b) {
                     const double sum = block_sum(b);
                     if (RB > 0) reg_set(gr, b, sqrt(sum / (double)fs), lane);
@@ -628,6 +651,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
             const double thr = p25 * 1.5;
             // Python max(new, MIN): MIN only if MIN > new
             st.threshold = (g.min_threshold > thr) ? g.min_threshold : thr;
+        } else if (g.compact && !(EWK_GATE_ABLATE & 1)) {
+            // filling a compact ring: keep this block's RMS now (its samples will not all
+            // be in the sample ring when the reference ring first fills)
+            const int b = p0 / fs;
+            const double v = sqrt(pw_sumsq([&](int c0) { return LdsSrc{stage + c0}; }, fs, tbf, tbr, lane, val) /
+                                  (double)fs);
+            if (RB > 0) reg_set(gr, b, v, lane);
+            else if (lane == 0) grms[b] = v;
         }
         GT_TS(q2);
         GT_ACC(2, q1, q2);
@@ -641,12 +672,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
                 const float* base = stage + (fs - nl);
                 sum = pw_sumsq([&](int c0) { return LdsSrc{base + c0}; }, nl, tlf, tlr, lane, val);
             } else {
-                int first = st.pointer - nl;
-                if (first < 0) first += R;
+                int first = st.spos - nl;
+                if (first < 0) first += Rs;
                 sum = pw_sumsq([&](int c0) {
                     int f = first + c0;
-                    if (f >= R) f -= R;
-                    return RingSrc{ring, f, R};
+                    if (f >= Rs) f -= Rs;
+                    return RingSrc{ring, f, Rs};
                 }, nl, tlf, tlr, lane, val);
             }
             const double rms = sqrt(sum / (double)nl);
@@ -709,8 +740,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
                         int64_t stop = nreq - e;   // python a[:len-e]
                         if (stop < 0) { stop += nreq; if (stop < 0) stop = 0; }
                         if (stop > nreq) stop = nreq;
-                        int64_t start = (int64_t)st.pointer - nreq;
-                        if (start < 0) start += R;
+                        // (the host sizes a compact ring for the longest possible request)
+                        int64_t start = (int64_t)st.spos - nreq;
+                        if (start < 0) start += Rs;
                         ewk_event ev;
                         ev.stream = s;
                         ev.length = (int32_t)stop;
@@ -737,7 +769,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
     }
     GT_TS(q_loop);
     GT_ACC(4, q_loaded, q_loop);
-    if (RB > 0 && st.filled) {
+    if (RB > 0 && (st.filled || g.compact)) {
 #pragma unroll
         for (int j = 0; j < RBn; ++j) {
             const int i = lane + 64 * j;
@@ -778,7 +810,7 @@ hipError_t launch_gate(const GateArgs& g, hipStream_t s) {
     const bool dma = EWK_GATE_DMA && g.pcm16 == nullptr && g.stage >= g.block && g.stage >= nl;
     // 16-B pieces: every tick row 16-B aligned, whole 4-sample groups that never straddle the ring wrap
     const bool dma4 = dma && EWK_GATE_DMA >= 2 && g.block % 4 == 0 && g.block <= 256 * kDma4Chunks &&
-                      g.stride % 4 == 0 && g.tick_stride % 4 == 0 && g.ring_len % 4 == 0 &&
+                      g.stride % 4 == 0 && g.tick_stride % 4 == 0 && g.ring_len % 4 == 0 && g.sring_len % 4 == 0 &&
                       ((uintptr_t)g.pcm & 15) == 0;
     if (g.n_blocks <= 128) {
         if (dma4) hipLaunchKernelGGL((k_gate_ticks<2, 2>), dim3(grid), dim3(256), lds, s, g);

@@ -29,7 +29,7 @@ extern "C" {
 #endif
 
 #define EWK_N_MFCC 20
-#define EWK_ABI_VERSION 1
+#define EWK_ABI_VERSION 2
 
 #define EWK_OK 0
 #define EWK_EINVAL (-1)       /* bad parameter            -> ValueError            */
@@ -60,7 +60,15 @@ typedef struct ewk_config {
     int32_t sample_rate;          /* 16000  SoundBuffer.FREQUENCY                  */
     int32_t buffer_seconds;       /* 10     DEFAULT_BUFFER_SECONDS                 */
     int32_t block;                /* 1600   samples per callback == per tick       */
-    int32_t reserved0;
+    int32_t ring_samples;         /* 0 = buffer_seconds * sample_rate (the reference ring).
+                                     Otherwise samples kept per stream for segment reads: a
+                                     compact ring with the same decisions and scores (block
+                                     RMSs are kept per block as they arrive), for configs whose
+                                     block divides the reference ring; must hold the longest
+                                     possible segment request (max speech + post silence + one
+                                     tick + padding) plus one tick, else EWK_EINVAL.  Saves HBM
+                                     per stream (10 s -> 3 s: 640 KB -> 192 KB); ewk_read_last
+                                     fails (EWK_EINVAL) for more than ring_samples. */
     double tick_seconds;          /* 0.1    time.sleep(0.1) in _detect_word        */
     double pre_speech_silence;    /* 0.8    DEFAULT_PRE_SPEECH_SILENCE             */
     double speech_duration_min;   /* 0.3    DEFAULT_SPEECH_DURATION_MIN            */
@@ -166,7 +174,11 @@ int ewk_push_many(ewk_engine* e, const float* pcm, int64_t stride, int64_t tick_
 int ewk_push_pcm16(ewk_engine* e, const int16_t* pcm, int64_t stride, int32_t flags);
 int ewk_push_many_pcm16(ewk_engine* e, const int16_t* pcm, int64_t stride, int64_t tick_stride,
                         int32_t n_ticks, int32_t flags);
-/* Drain up to `cap` queued events (waits for every push so far). */
+/* Drain every queued event (waits for every push so far), sorted by (tick, stream).
+ * If more than `cap` are queued nothing is consumed and EWK_EINVAL is returned (poll
+ * again with a larger buffer).  If a bank overflowed (more than max(4096, 4 * n_streams)
+ * events between polls) its events are dropped, the queue is re-armed so later pushes
+ * keep working, and EWK_ENOMEM reports the loss. */
 int ewk_poll(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out);
 /* Pipelined drain: returns the events of the pushes made before the previous
  * ewk_poll_lagged call, without waiting for the pushes made since -- the GPU

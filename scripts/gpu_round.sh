@@ -6,7 +6,7 @@ MODE=${1:-all}
 export EWK_RAW=${EWK_RAW:-/tmp/ewk_raw_$$}   # raw PMC csvs stay on the box (gpurun_out is capped at 64 MiB)
 ok_or_testfail() { local rc=$1; [ $rc -eq 0 ] || [ $rc -eq 1 ]; }
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
-  timeout -k 10 900 python -m pytest tests -q -m gpu -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 1000 python -u -m pytest tests -v -m gpu -x -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
   ok_or_testfail $rc || exit $rc
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1

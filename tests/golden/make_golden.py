@@ -245,6 +245,16 @@ STREAMS = [
     ("tight_windows", dict(seed=1239, n_words=6, sigma=1e-3, gain=1.2),
      {"pre_speech_silence": 0.5, "speech_duration_min": 0.69, "speech_duration_max": 1.38,
       "post_speech_silence": 0.3}),
+    # level-2 rejects, near-threshold scores, negative-similarity NaNs and a segment
+    # straddling the ring wrap (tick 311: first sample before the physical end)
+    ("rejects_gain3", dict(seed=1300, n_words=8, sigma=1e-3, gain=3.0, kinds=["hp", "white", "hp_near", "hp"]), {}),
+    ("rejects_gain5", dict(seed=1300, n_words=8, sigma=1e-3, gain=5.0, kinds=["hp", "white", "hp_near", "hp"]), {}),
+    # segments longer than max_segment_seconds: the reference skips level 2 (wakeword.py:1113-1118)
+    ("skip_long", dict(seed=1301, n_words=6, sigma=1e-3, gain=1.0, kinds=["long", "word", "long"]),
+     {"speech_duration_max": 3.5}),
+    # frame_size 512: 312 physical blocks, unaligned pointer (wakeword.py:472-486)
+    ("frame512_bursts", dict(seed=1302, n_words=8, sigma=1e-3, gain=1.0, kinds=["burst", "hp", "burst", "word"],
+                             block=512), {"block": 512, "speech_duration_max": 6.0}),
 ]
 
 

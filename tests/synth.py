@@ -26,8 +26,14 @@ def load_word() -> np.ndarray:
 
 
 def make_stream(seed: int, n_words: int = 8, prefill: float = 10.0, sigma: float = 1e-3,
-                gain: float = 1.0, distractors: bool = False, block: int = 1600):
-    """Returns (pcm float32 padded to a multiple of `block`, list of (start, kind))."""
+                gain: float = 1.0, distractors: bool = False, block: int = 1600, kinds=None):
+    """Returns (pcm float32 padded to a multiple of `block`, list of (start, kind)).
+
+    kinds: explicit event kinds, cycled (no random kind draw), including the level-2
+    rejects: "hp" (differenced white noise x 0.1: scores ~68 < 75), "hp_near" (x 0.05:
+    ~73-75, near the threshold), "white" (loud white noise: negative similarity -> NaN)
+    "burst" (the word's first 0.3 s) and "long" (a 3.2 s harmonic hum: longer than max_segment_seconds when the gate's
+    speech_duration_max allows it, so the reference skips level 2, wakeword.py:1113-1118)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     word = load_word()
     parts = [rng.normal(0.0, sigma, int(prefill * SR)).astype(np.float32)]
@@ -38,12 +44,26 @@ def make_stream(seed: int, n_words: int = 8, prefill: float = 10.0, sigma: float
         parts.append(gap)
         pos += len(gap)
         kind = "word"
-        if distractors:
+        if kinds:
+            kind = kinds[i % len(kinds)]
+        elif distractors:
             kind = ["word", "tone880", "noise", "reversed"][int(rng.integers(0, 4))]
         if kind == "word":
             ev = word * np.float32(gain)
         elif kind == "reversed":
             ev = word[::-1] * np.float32(gain)
+        elif kind in ("hp", "hp_near"):
+            ev = (np.diff(rng.standard_normal(len(word) + 1)) * (0.1 if kind == "hp" else 0.05) * gain)
+            ev = ev.astype(np.float32)
+        elif kind == "burst":
+            ev = word[:4800] * np.float32(gain)
+        elif kind == "white":
+            ev = (rng.standard_normal(len(word)) * 0.8 * gain).astype(np.float32)
+        elif kind == "long":
+            t = np.arange(int(3.2 * SR)) / SR
+            env = np.minimum(1.0, np.minimum(t, t[-1] - t) / 0.05)
+            ev = ((0.3 * np.sin(2 * np.pi * 150 * t) + 0.2 * np.sin(2 * np.pi * 500 * t)
+                   + 0.1 * np.sin(2 * np.pi * 1500 * t)) * env * gain).astype(np.float32)
         elif kind == "tone880":
             t = np.arange(len(word)) / SR
             env = np.sin(np.pi * t / t[-1]) ** 0.5
@@ -140,4 +160,19 @@ def matcher_cases():
         cases.append((f"ragged_{i:02d}", seg))
     cases.append(("silence_6400", np.zeros(6400, np.float32)))
     cases.append(("silence_16000", np.zeros(16000, np.float32)))
+    # audible level-2 rejects and near-threshold cases (differenced / twice-differenced
+    # white noise: high-passed spectra score 0-75 against the word; loud white noise
+    # drives the similarity negative -> NaN)
+    rng = np.random.Generator(np.random.PCG64(4242))
+    n = len(word)
+    for g in (0.03, 0.04, 0.045, 0.05, 0.055, 0.06, 0.1, 0.2, 0.5, 1.0):
+        cases.append((f"hp_noise_{g:g}", (np.diff(rng.standard_normal(n + 1)) * g).astype(np.float32)))
+    for g in (0.05, 0.2):
+        cases.append((f"hp2_noise_{g:g}", (np.diff(rng.standard_normal(n + 2), 2) * g).astype(np.float32)))
+    for g in (0.5, 1.5):
+        cases.append((f"white_{g:g}", (rng.standard_normal(n) * g).astype(np.float32)))
+    # a word buried in high-passed noise (mixtures near the decision)
+    for g in (0.3, 0.6):
+        cases.append((f"word_in_hp_{g:g}", (word * np.float32(g) + np.diff(rng.standard_normal(n + 1)) * 0.08)
+                      .astype(np.float32)))
     return [(n, np.ascontiguousarray(x, dtype=np.float32)) for n, x in cases]

@@ -39,7 +39,7 @@ def test_defaults_are_reference_constants():
         (0.8, 0.3, 2.0, 0.4)
     assert (c.padding, c.max_segment_seconds, c.similarity_threshold) == (0.05, 3.0, 75.0)
     assert (c.min_threshold, c.initial_threshold, c.tick_seconds) == (0.005, 0.01, 0.1)
-    assert _lib.load().ewk_abi_version() == 1
+    assert _lib.load().ewk_abi_version() == 2
 
 
 def test_no_silent_cpu_fallback():
@@ -55,3 +55,17 @@ def test_invalid_config_raises_valueerror_before_device_check():
     from easywakeword_amd import Engine
     with pytest.raises(ValueError, match="speech_duration_min must be <= speech_duration_max"):
         Engine(speech_duration_min=2.0, speech_duration_max=1.0)
+
+
+@pytest.mark.parametrize("cfg, msg", [
+    (dict(ring_samples=19200), "longest segment request"),         # < 2.55 s + one tick
+    (dict(ring_samples=48000, block=512), "block to divide"),     # 160000 % 512 != 0
+    (dict(ring_samples=48000 + 800), "block to divide"),           # not a whole number of ticks
+    (dict(ring_samples=-1), "ring_samples must be in"),
+    (dict(ring_samples=170000), "ring_samples must be in"),        # larger than the reference ring
+])
+def test_compact_ring_config_validated_before_device_check(cfg, msg):
+    """ewk_config.ring_samples (compact sample rings) is checked on the host, GPU or not."""
+    from easywakeword_amd import StreamEngine
+    with pytest.raises(ValueError, match=msg):
+        StreamEngine(4, **cfg)

@@ -71,7 +71,8 @@ def test_gate_oracle_reproduces_reference_traces(rec):
     g = rec["gate"]
     cfg = GateConfig(pre_speech_silence=g["pre_speech_silence"], speech_duration_min=g["speech_duration_min"],
                      speech_duration_max=g["speech_duration_max"], post_speech_silence=g["post_speech_silence"],
-                     reentry_timeout=g.get("reentry_timeout"))
+                     reentry_timeout=g.get("reentry_timeout"), block=g.get("block", 1600),
+                     buffer_seconds=g.get("buffer_seconds", 10))
     det = run_stream(pcm, cfg)
     evs = [e for e in det.events if not e.skipped]
     assert [(e.tick, e.length) for e in evs] == [(e["tick"], e["length"]) for e in rec["events"]]
