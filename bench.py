@@ -15,15 +15,20 @@ high-passed noise burst (scores ~70, below the default 75), so both decisions
 occur.  A step = one scorer pass over the
 whole batch: MFCC (stft+mel+log+top_db+DCT), mean/std, cosine score, match,
 and the fp64 re-score of near-threshold segments.  For N>1 the step also
-all-gathers every rank's (score, match) to rank 0 over RCCL -- the gather of
-positive detections that feeds the optional Whisper confirm.
-Streams shard across ranks (weak scaling).
+gathers the matched segments' (id, score) records to rank 0 over RCCL -- the
+positives that feed the optional Whisper confirm: device-side
+compaction, an all_gather of the counts, point-to-point records.  Streams shard
+across ranks (weak scaling).
 
 Extra fields: ``roofline`` (dominant kernel k_score_f32, 640 algorithmic bytes
 per MFCC frame, HIP-event timed), ``cpu_baseline`` (oracle/mfcc_ref.py, the
 librosa-0.11 restatement, on rank 0 at N=1 only, time-bounded sample),
 ``streaming`` (configs[2]: 8192 streams through the full level-1 + level-2
-engine, per-tick launches, real-time capacity).
+engine, one tick per push), ``streaming_100k`` (131,072 resident streams with the
+reference's 10 s rings) and ``streaming_max`` (as many resident streams as HBM holds
+with compact 3 s sample rings, default 1,048,576): measured ms per tick, never
+extrapolated -- ``streams_realtime`` is the resident count when every tick of every
+stream finished inside the 100 ms tick budget.
 """
 from __future__ import annotations
 
@@ -381,9 +386,12 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
     base = pcm.data_ptr()
 
     events = []
-    gathered = [0]
-    if world > 1:
-        from easywakeword_amd.shard import gather_positives
+    col = None
+    if world > 1:   # level-3 feed: positives to rank 0 every second, PCM of the newest 64 per rank
+        from easywakeword_amd.shard import PositiveCollector
+        col = PositiveCollector(first_stream, cdev, every=10, audio_cap=64,
+                                audio_fn=(se.normalize_events_device if cdev.type == "cuda" else
+                                          lambda e: [a.cpu() for a in se.normalize_events_device(e)]))
 
     def run(t0, nt, per_call, lagged=False):
         t = t0
@@ -397,14 +405,9 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
             # the host consumes detections every call; lagged: tick t-1's events while the GPU runs tick t
             ev = se.poll(lagged=lagged)
             events.append(ev)
-            if world > 1:                   # positives of every rank -> rank 0 (level-3 input)
-                pos = ev[(ev["match"] != 0) & ((ev["flags"] & 1) == 0)]
-                rec = np.stack([pos["stream"].astype(np.int64) + first_stream, pos["tick"].astype(np.int64),
-                                pos["length"].astype(np.int64), pos["score"].view(np.int64)], axis=1) \
-                    if len(pos) else np.zeros((0, 4), np.int64)
-                out, _ = gather_positives(torch.from_numpy(rec).to(cdev))
-                if out is not None:
-                    gathered[0] += int(out.shape[0])
+            if col is not None:             # positives of every rank -> rank 0 (level-3 input)
+                col.add(ev)
+                col.tick(n)
             t += n
         return t
 
@@ -452,8 +455,11 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
            "events": int(len(real)), "matches": int(real["match"].sum()) if len(real) else 0,
            "mfcc_frames": int((1 + real["length"].astype(np.int64) // HOP).sum()) if len(real) else 0}
     out["mfcc_frames_per_s"] = out["mfcc_frames"] / wall   # gated segments scored, over the timed ticks
-    if world > 1:
-        out["positives_gathered_to_rank0"] = gathered[0]
+    if col is not None:
+        col.flush()
+        out["positives_gathered_to_rank0"] = col.gathered
+        out["positive_pcm_gathered_to_rank0"] = col.gathered_audio
+        out["gather"] = "every 10 ticks: counts all_gather + point-to-point records and normalised PCM to rank 0"
     if confirm_batch > 0:   # config 5: level 3 on the latest positives still in the rings
         out["confirm"] = confirm_bench(se, ev_latest, t, confirm_batch, dev)
     se.close()
@@ -499,14 +505,14 @@ def main():
     torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
     assert sh != 0
-    if world > 1:
-        from easywakeword_amd.shard import DecisionGather
-        gather = DecisionGather(score.to(cdev), match.to(cdev))   # tests/test_dist_gloo.py: same code over gloo
+    if world > 1:   # positives only: device compaction, counts all_gather, P2P records (tests/test_dist_gloo.py)
+        from easywakeword_amd.shard import MatchGather
+        gather = MatchGather(n_seg, rank * n_seg, cdev)
 
     def step():
         eng.score_device(pcm.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n_seg, mean.data_ptr(),
                          std.data_ptr(), score.data_ptr(), match.data_ptr(), sh)
-        if world > 1:   # gather every rank's decisions to all (rank 0 runs the confirm stage)
+        if world > 1:   # the matched segments' (id, score) records -> rank 0 (the confirm stage's input)
             gather(score.to(cdev), match.to(cdev))
 
     torch.cuda.synchronize()
@@ -585,7 +591,8 @@ def main():
             "frames_per_step_per_gpu": frames,
             "frames_per_step_all_gpus": int(frames_all.item()),
             "global_batch": n_seg * world,
-            "parallelism": f"dp{world} (stream shards, RCCL all-gather of decisions)" if world > 1 else "dp1",
+            "parallelism": f"dp{world} (stream shards, RCCL gather of positive records to rank 0)" if world > 1
+                           else "dp1",
         },
         "roofline": {
             "bound": "hbm",

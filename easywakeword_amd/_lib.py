@@ -40,7 +40,7 @@ EXPORTS = [
     "ewk_read_segment", "ewk_reset_streams", "ewk_set_similarity_threshold",
     "ewk_profile_enable", "ewk_profile_read",
     "ewk_push_pcm16", "ewk_push_many_pcm16", "ewk_normalize_segments", "ewk_normalize_events",
-    "ewk_decode_pcm16", "ewk_poll_lagged",
+    "ewk_decode_pcm16", "ewk_poll_lagged", "ewk_runtime_info",
 ]
 
 
@@ -113,6 +113,7 @@ def load():
             "ewk_last_error": (C.c_char_p, []),
             "ewk_abi_version": (C.c_int, []),
             "ewk_device_count": (C.c_int, []),
+            "ewk_runtime_info": (C.c_int, [C.c_char_p, C.c_int32, _i32p]),
             "ewk_create": (C.c_int, [C.POINTER(_P), C.c_int, C.c_int32, C.POINTER(EwkConfig)]),
             "ewk_destroy": (None, [_P]),
             "ewk_sync": (C.c_int, [_P]),
@@ -169,6 +170,17 @@ def default_config(**overrides) -> EwkConfig:
             raise TypeError(f"unknown config field {k!r}")
         setattr(cfg, k, v)
     return cfg
+
+
+def runtime_info() -> dict:
+    """The HIP runtime libewk.so's calls bind to: {"path": file defining hipLaunchKernel,
+    "hip_version": hipRuntimeGetVersion or -1, "torch_bundled": path inside a torch wheel}."""
+    buf = C.create_string_buffer(4096)
+    v = C.c_int32(-1)
+    check(load().ewk_runtime_info(buf, len(buf), C.byref(v)))
+    path = buf.value.decode(errors="replace")
+    return {"path": path, "hip_version": int(v.value),
+            "torch_bundled": f"{os.sep}torch{os.sep}lib{os.sep}" in path}
 
 
 def device_count() -> int:

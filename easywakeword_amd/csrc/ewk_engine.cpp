@@ -1,5 +1,6 @@
 // ewk_engine.cpp -- the C ABI (include/ewk.h): engine lifetime, device memory,
 // the level-2 batch scorer entry points and the level-1+2 streaming tick path.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
@@ -233,6 +234,26 @@ void ewk_default_config(ewk_config* c) {
 
 const char* ewk_last_error(void) { return g_err.c_str(); }
 int ewk_abi_version(void) { return EWK_ABI_VERSION; }
+
+int ewk_runtime_info(char* path, int32_t cap, int32_t* hip_version) {
+    // the definition hipLaunchKernel resolved to for this library: with RTLD_GLOBAL
+    // interposition (e.g. torch's bundled runtime loaded first) it is not the
+    // libamdhip64.so.7 libewk.so was linked against
+    Dl_info info;
+    memset(&info, 0, sizeof(info));
+    const void* sym = reinterpret_cast<const void*>(&hipLaunchKernel);
+    if (!dladdr(sym, &info) || !info.dli_fname) return fail(EWK_EHIP, "dladdr(hipLaunchKernel) failed");
+    if (path && cap > 0) {
+        strncpy(path, info.dli_fname, (size_t)cap - 1);
+        path[cap - 1] = 0;
+    }
+    if (hip_version) {
+        int v = -1;
+        if (hipRuntimeGetVersion(&v) != hipSuccess) v = -1;
+        *hip_version = v;
+    }
+    return EWK_OK;
+}
 
 int ewk_device_count(void) {
     int n = 0;

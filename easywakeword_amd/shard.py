@@ -3,12 +3,27 @@
 Streams are independent, so they are partitioned across ranks with no data-path
 collective (weak scaling): rank r owns a contiguous block of streams, gates them
 and scores their segments on its own GPU.  The only exchange is the gather of
-level-2 decisions (score, match) to every rank -- the input of the optional
-level-3 confirm, which the reference runs once per detection
-(wakeword.py:1120-1130).  Over RCCL (backend "nccl") on MI355X; the same code
-runs over gloo on CPU tensors in the tests.
+POSITIVE detections to one rank -- the input of the optional level-3 confirm,
+which the reference runs once per detection (wakeword.py:1120-1130):
+
+* ``MatchGather``       (batch scorer step) device-side compaction of the matched
+                        segments' (id, score) records, no host sync before the
+                        collectives, then ``gather_positives``;
+* ``PositiveCollector`` (streaming) accumulates each tick's polled positives and
+                        gathers them every ``every`` ticks, with the level-3 input
+                        PCM of up to ``audio_cap`` of them per rank;
+* ``gather_positives``  one all_gather of the per-rank counts (three int64 per
+                        rank), then point-to-point sends of each rank's records and
+                        packed PCM to ``dst`` (batch_isend_irecv), sized by the counts.
+
+Over RCCL (backend "nccl") on MI355X; the same code runs over gloo on CPU tensors
+in the tests (tests/test_dist_gloo.py).
 """
 from __future__ import annotations
+
+from typing import Callable, Optional
+
+import numpy as np
 
 
 def shard_streams(n_streams: int, rank: int, world: int) -> tuple[int, int]:
@@ -22,98 +37,156 @@ def shard_streams(n_streams: int, rank: int, world: int) -> tuple[int, int]:
     return start, base + (1 if rank < extra else 0)
 
 
-class DecisionGather:
-    """All-gather of every rank's per-segment (score, match) arrays.
-
-    Buffers are allocated once for a fixed per-rank segment count (the bench's
-    step shape) so the collective runs without allocation inside the timed loop.
-    `__call__` returns the world's scores and matches concatenated in rank order.
-    """
-
-    def __init__(self, score, match, group=None):
-        import torch.distributed as dist
-        self._dist = dist
-        self.group = group
-        self.world = dist.get_world_size(group)
-        self.score_parts = [score.new_empty(score.shape) for _ in range(self.world)]
-        self.match_parts = [match.new_empty(match.shape) for _ in range(self.world)]
-
-    def __call__(self, score, match):
-        self._dist.all_gather(self.score_parts, score, group=self.group)
-        self._dist.all_gather(self.match_parts, match, group=self.group)
-        return self.score_parts, self.match_parts
-
-    def concatenated(self):
-        import torch
-        return torch.cat(self.score_parts), torch.cat(self.match_parts)
-
-
-def gather_positives(records, audio=None, group=None, dst: int = 0):
+def gather_positives(records, audio=None, count=None, group=None, dst: int = 0):
     """Gather every rank's positive detections to rank `dst`.
 
     records: [n, k] int64 tensor on this rank, k >= 3 with column 2 = segment length
              (the event fields: stream, tick, length, score bits, ...);
-    audio:   optional list of n 1-D float tensors (the segments' PCM, lengths as in column 2).
-    Collectives: an all_gather of the per-rank counts (and PCM totals), an all_gather
-    of the count-padded records, then point-to-point sends of each rank's packed PCM
-    to `dst` (batch_isend_irecv).  Returns (records, audio list) on `dst`, (None, None)
-    elsewhere.  The tensors must live where the backend expects them (CUDA for RCCL,
-    CPU for gloo).
+    count:   optional 0-d/1-element int64 tensor on the records' device: only
+             records[:count] are sent (device-side compaction leaves the count on the
+             GPU; it is read once, with the other ranks' counts, after the all_gather);
+    audio:   optional list of 1-D float tensors, the PCM of the FIRST len(audio)
+             records (lengths as in their column 2).
+    Collectives: an all_gather of (count, PCM total, PCM records) per rank, then
+    point-to-point sends of each rank's records and packed PCM to `dst`.
+    Returns (records, audio list) on `dst`, (None, None) elsewhere; the tensors must
+    live where the backend expects them (CUDA for RCCL, CPU for gloo).
     """
     import torch
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    n = records.shape[0]
+    dev = records.device
     k = records.shape[1] if records.dim() == 2 else 0
     flat = torch.cat([a.reshape(-1) for a in audio]) if audio else None
     total = 0 if flat is None else flat.numel()
-    meta = torch.tensor([n, total], dtype=torch.int64, device=records.device)
-    metas = [torch.empty_like(meta) for _ in range(world)]
-    dist.all_gather(metas, meta, group=group)
-    counts = [int(m[0]) for m in metas]
-    totals = [int(m[1]) for m in metas]
-    cap = max(1, max(counts))
-    padded = records.new_zeros((cap, k))
-    if n:
-        padded[:n] = records
-    parts = [torch.empty_like(padded) for _ in range(world)]
-    dist.all_gather(parts, padded, group=group)
-    out_rec = torch.cat([parts[r][:counts[r]] for r in range(world)]) if rank == dst else None
+    n_audio = len(audio) if audio else 0
+    n = count.reshape(1).to(torch.int64) if count is not None else \
+        torch.tensor([records.shape[0]], dtype=torch.int64, device=dev)
+    meta = torch.cat([n, torch.tensor([total, n_audio], dtype=torch.int64, device=dev)])
+    # a collective first: later point-to-point calls may then involve a subset of ranks
+    parts = [torch.empty_like(meta) for _ in range(world)]
+    dist.all_gather(parts, meta, group=group)
+    m = torch.stack(parts).cpu().tolist()           # the one host sync of a gather
+    counts, totals, n_aud = [r[0] for r in m], [r[1] for r in m], [r[2] for r in m]
+    ops, rec_bufs, pcm_bufs = [], {}, {}
+    dtype = flat.dtype if flat is not None else torch.float64
+    if rank == dst:
+        for r in range(world):
+            if r == dst:
+                continue
+            if counts[r]:
+                rec_bufs[r] = torch.empty((counts[r], k), dtype=records.dtype, device=dev)
+                ops.append(dist.P2POp(dist.irecv, rec_bufs[r], r, group=group))
+            if totals[r]:
+                pcm_bufs[r] = torch.empty(totals[r], dtype=dtype, device=dev)
+                ops.append(dist.P2POp(dist.irecv, pcm_bufs[r], r, group=group))
+        rec_bufs[dst] = records[:counts[dst]]
+        if flat is not None:
+            pcm_bufs[dst] = flat
+    else:
+        if counts[rank]:
+            ops.append(dist.P2POp(dist.isend, records[:counts[rank]].contiguous(), dst, group=group))
+        if total:
+            ops.append(dist.P2POp(dist.isend, flat, dst, group=group))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    if rank != dst:
+        return None, None
+    out_rec = torch.cat([rec_bufs[r] for r in range(world) if counts[r]]) if sum(counts) else \
+        records.new_zeros((0, k))
     out_audio = None
     if audio is not None:
-        ops, bufs = [], {}
-        if rank == dst:
-            for r in range(world):
-                if r == dst or totals[r] == 0:
-                    continue
-                bufs[r] = torch.empty(totals[r], dtype=flat.dtype if flat is not None else torch.float32,
-                                      device=records.device)
-                ops.append(dist.P2POp(dist.irecv, bufs[r], r, group=group))
-            if flat is not None:
-                bufs[dst] = flat
-        elif total:
-            ops.append(dist.P2POp(dist.isend, flat, dst, group=group))
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
-        if rank == dst:
-            out_audio = []
-            for r in range(world):
-                lens = [int(x) for x in parts[r][:counts[r], 2]] if counts[r] else []
-                buf, o = bufs.get(r), 0
-                for ln in lens:
-                    out_audio.append(buf[o:o + ln])
-                    o += ln
+        out_audio = []
+        for r in range(world):
+            if not n_aud[r]:
+                continue
+            lens = [int(x) for x in rec_bufs[r][:n_aud[r], 2].tolist()]
+            buf, o = pcm_bufs[r], 0
+            for ln in lens:
+                out_audio.append(buf[o:o + ln])
+                o += ln
     return out_rec, out_audio
 
 
-def positives(scores, matches, first_stream_of_rank, segments_per_stream: int):
-    """Global (stream, segment) ids of the gathered matches -- what rank 0 hands to the confirm stage."""
-    import torch
-    out = []
-    for r, (s, m) in enumerate(zip(scores, matches)):
-        idx = torch.nonzero(m.to(torch.bool), as_tuple=False).flatten()
-        for i in idx.tolist():
-            out.append((first_stream_of_rank[r] + i // segments_per_stream, i % segments_per_stream,
-                        float(s[i])))
-    return out
+class MatchGather:
+    """Batch scorer step on N ranks: the matched segments' records go to `dst`.
+
+    Device-side compaction into a persistent [n_seg, 2] int64 buffer (column 0 =
+    global segment id first_id + i, column 1 = the float64 score's bits), with the
+    count left on the device: no host sync until the counts' all_gather, and only
+    positives cross xGMI (not the per-segment score/match arrays).
+    """
+
+    def __init__(self, n_seg: int, first_id: int, device, group=None, dst: int = 0):
+        import torch
+        self.n_seg, self.first_id, self.group, self.dst = n_seg, first_id, group, dst
+        self.buf = torch.zeros((n_seg + 1, 2), dtype=torch.int64, device=device)   # row n_seg: discard slot
+        self.ids = torch.arange(first_id, first_id + n_seg, dtype=torch.int64, device=device)
+
+    def compact(self, score, match):
+        """(records [n_seg + 1, 2], count [1]) with records[:count] the matches in index order."""
+        import torch
+        m = match.reshape(-1).to(torch.int64)
+        pos = torch.cumsum(m, 0) - 1
+        tgt = torch.where(m.bool(), pos, torch.full_like(pos, self.n_seg))
+        vals = torch.stack([self.ids, score.reshape(-1).to(torch.float64).view(torch.int64)], 1)
+        self.buf.index_copy_(0, tgt, vals)
+        return self.buf, pos[-1:] + 1
+
+    def __call__(self, score, match):
+        rec, cnt = self.compact(score, match)
+        return gather_positives(rec, count=cnt, group=self.group, dst=self.dst)[0]
+
+
+class PositiveCollector:
+    """Streaming level-3 feed on N ranks: each tick's polled positives (match, not
+    skipped) are kept on the host and gathered to `dst` every `every` ticks, records
+    {global stream, tick, length, score bits} plus the level-3 input PCM of the newest
+    `audio_cap` of them per rank (`audio_fn(events) -> list of 1-D tensors`, e.g.
+    StreamEngine.normalize_events_device: the normalised audio, wakeword.py:1019-1025,
+    straight from the rings)."""
+
+    def __init__(self, first_stream: int, device, every: int = 10, audio_cap: int = 64,
+                 audio_fn: Optional[Callable] = None, group=None, dst: int = 0):
+        self.first_stream, self.device, self.every, self.audio_cap = first_stream, device, every, audio_cap
+        self.audio_fn, self.group, self.dst = audio_fn, group, dst
+        self.pending = []
+        self.ticks = 0
+        self.gathered = 0
+        self.gathered_audio = 0
+
+    def add(self, events: np.ndarray) -> None:
+        pos = events[(events["match"] != 0) & ((events["flags"] & 1) == 0)]
+        if len(pos):
+            self.pending.append(pos)
+
+    def tick(self, n: int = 1):
+        """Count n ticks; gathers when `every` ticks have passed (returns flush()'s result)."""
+        self.ticks += n
+        if self.ticks >= self.every:
+            return self.flush()
+        return None, None
+
+    def flush(self):
+        import torch
+        self.ticks = 0
+        ev = np.concatenate(self.pending) if self.pending else None
+        self.pending = []
+        if ev is None or not len(ev):
+            rec = np.zeros((0, 4), np.int64)
+            ev = None
+        else:
+            # newest first, so the PCM rides with the first audio_cap records
+            ev = ev[np.lexsort((ev["stream"], -ev["tick"]))]
+            rec = np.stack([ev["stream"].astype(np.int64) + self.first_stream, ev["tick"].astype(np.int64),
+                            ev["length"].astype(np.int64), ev["score"].astype(np.float64).view(np.int64)], axis=1)
+        audio = None
+        if self.audio_fn is not None:
+            audio = list(self.audio_fn(ev[:self.audio_cap])) if ev is not None and self.audio_cap > 0 else []
+        out_rec, out_audio = gather_positives(torch.from_numpy(rec).to(self.device), audio=audio,
+                                              group=self.group, dst=self.dst)
+        if out_rec is not None:
+            self.gathered += int(out_rec.shape[0])
+            self.gathered_audio += len(out_audio) if out_audio is not None else 0
+        return out_rec, out_audio

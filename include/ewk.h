@@ -116,6 +116,14 @@ const char* ewk_last_error(void);
 int ewk_abi_version(void);
 /* number of visible HIP devices (0 when none); never fails */
 int ewk_device_count(void);
+/* Which HIP runtime this library's calls bind to: the file that defines the
+ * hipLaunchKernel it resolved (dladdr) and hipRuntimeGetVersion (-1 if unavailable).
+ * libewk.so links the system ROCm runtime (libamdhip64.so.7); a process that loaded
+ * another copy first with RTLD_GLOBAL (PyTorch-ROCm wheels bundle one) binds that
+ * copy instead -- then both libraries share ONE runtime and device pointers and
+ * hipStream_t values pass between them.  Two runtimes that each own the device are
+ * never in use at once. */
+int ewk_runtime_info(char* path, int32_t cap, int32_t* hip_version);
 
 /* Engine: device index, number of concurrent streams (0 = scorer only). */
 int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config* cfg);

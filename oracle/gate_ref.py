@@ -296,3 +296,15 @@ def run_stream(pcm: np.ndarray, cfg: GateConfig, keep_audio: bool = True) -> Det
     for k in range(nb):
         det.push_tick(pcm[k * cfg.block:(k + 1) * cfg.block])
     return det
+
+
+def normalize_level3(audio: np.ndarray) -> np.ndarray:
+    """WakeWord._transcribe_audio's input normalisation (wakeword.py:1019-1025) on the
+    float64 segment: remove the mean, scale to max |y| = 1 when non-zero, x1.5, clip."""
+    a = np.asarray(audio, dtype=np.float64)
+    a = a - np.mean(a)
+    max_val = np.max(np.abs(a))
+    if max_val > 0:
+        a = a / max_val
+    a = a * 1.5
+    return np.clip(a, -1.0, 1.0)

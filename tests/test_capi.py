@@ -69,3 +69,19 @@ def test_compact_ring_config_validated_before_device_check(cfg, msg):
     from easywakeword_amd import StreamEngine
     with pytest.raises(ValueError, match=msg):
         StreamEngine(4, **cfg)
+
+
+def test_runtime_info_reports_the_bound_hip_runtime():
+    """ewk_runtime_info: torch's bundled runtime when torch was imported first (the
+    default of _lib.load), the system ROCm runtime in a torch-free process."""
+    import json
+    import subprocess
+    import sys
+    code = ("import json, sys; from easywakeword_amd import _lib; i = _lib.runtime_info(); "
+            "i['torch'] = 'torch' in sys.modules; print(json.dumps(i))")
+    env = dict(os.environ, EWK_NO_TORCH_PRELOAD="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, cwd=ROOT, timeout=120)
+    assert r.returncode == 0, r.stderr
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    assert not info["torch"] and not info["torch_bundled"]
+    assert os.path.basename(info["path"]).startswith("libamdhip64.so")

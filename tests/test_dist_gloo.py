@@ -1,9 +1,11 @@
-"""N>1 layout of the hot path on CPU: world_size-2 gloo, the same sharding and
-decision gather bench.py runs over RCCL (easywakeword_amd/shard.py).
+"""N>1 layout of the hot path on CPU: world_size 2 and 3 over gloo, the same sharding
+and positives gathers bench.py runs over RCCL (easywakeword_amd/shard.py).
 
-The per-rank scorer here is the oracle (CPU, test-only): the point is that the
-stream partition and the all-gather reproduce, on every rank, exactly the
-decisions a single process computes over all streams.
+The per-rank scorer / gate here is the oracle (CPU, test-only): the point is that
+the stream partition plus the gathers reproduce on rank 0 exactly the positives a
+single process finds over all streams -- batch decisions (MatchGather: device-side
+compaction, counts all_gather, point-to-point records) and the streaming level-3 feed
+(PositiveCollector: per-tick positives batched every K ticks, with the normalised PCM).
 """
 import os
 import socket
@@ -14,7 +16,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from easywakeword_amd.shard import DecisionGather, gather_positives, positives, shard_streams
+from easywakeword_amd.shard import MatchGather, PositiveCollector, gather_positives, shard_streams
 
 N_STREAMS = 5
 SEG_PER_STREAM = 3
@@ -58,21 +60,37 @@ def _score_streams(streams):
     return np.array(sc, np.float64), np.array(mt, np.uint8)
 
 
-def _worker(rank, world, port, q):
+def _run_world(target, world, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    for _ in range(world):
+        r, payload = q.get(timeout=300)
+        results[r] = payload
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return results
+
+
+def _init(rank, world, port):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _worker_match(rank, world, port, q):
+    _init(rank, world, port)
     try:
-        # equal shards so the fixed-shape all_gather applies (the bench's per-rank shape)
-        first, count = shard_streams(N_STREAMS + 1, rank, world)
+        first, count = shard_streams(N_STREAMS, rank, world)     # uneven shards
         sc, mt = _score_streams(range(first, first + count))
-        score, match = torch.from_numpy(sc), torch.from_numpy(mt)
-        g = DecisionGather(score, match)
-        parts_s, parts_m = g(score, match)
-        firsts = [shard_streams(N_STREAMS + 1, r, world)[0] for r in range(world)]
-        pos = positives(parts_s, parts_m, firsts, SEG_PER_STREAM)
-        all_s, all_m = g.concatenated()
-        q.put((rank, all_s.numpy(), all_m.numpy(), pos))
+        g = MatchGather(len(sc), first * SEG_PER_STREAM, torch.device("cpu"))
+        rec = g(torch.from_numpy(sc), torch.from_numpy(mt))
+        q.put((rank, None if rec is None else rec.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -90,25 +108,16 @@ def test_shard_streams_partition():
         shard_streams(-1, 0, 1)
 
 
-def test_gloo_world2_gather_matches_single_process():
-    world = 2
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    results = [q.get(timeout=300) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    ref_s, ref_m = _score_streams(range(N_STREAMS + 1))
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_match_gather_equals_single_process(world):
+    """Only the matched segments reach rank 0: (global segment id, score bits), in order."""
+    res = _run_world(_worker_match, world)
+    ref_s, ref_m = _score_streams(range(N_STREAMS))
     assert ref_m.any() and not ref_m.all()     # both decisions occur
-    for rank, s, m, pos in sorted(results, key=lambda r: r[0]):
-        np.testing.assert_array_equal(s, ref_s)   # same oracle, same inputs: bit-identical
-        np.testing.assert_array_equal(m, ref_m)
-        want = [(i // SEG_PER_STREAM, i % SEG_PER_STREAM) for i in np.nonzero(ref_m)[0]]
-        assert [(a, b) for a, b, _ in pos] == want
+    idx = np.nonzero(ref_m)[0]
+    want = np.stack([idx.astype(np.int64), ref_s[idx].view(np.int64)], 1)
+    np.testing.assert_array_equal(res[0], want)
+    assert all(res[r] is None for r in range(1, world))
 
 
 def _rank_positives(rank):
@@ -156,3 +165,99 @@ def test_gloo_world3_gather_positives_with_pcm():
     for a, b in zip(aud, want_aud):
         np.testing.assert_array_equal(a, b)
     assert results[1] == (None, None) and results[2] == (None, None)
+
+
+# ---------------------------------------------------------------- streaming level-3 feed
+STREAMS_S = 5
+EVERY = 10
+
+
+def _stream_audio():
+    import synth
+    pcms = [synth.make_stream(seed=6100 + s, n_words=5, sigma=1e-3, gain=[1.0, 3.0, 0.6, 2.0, 1.2][s],
+                              kinds=[["word", "hp"], ["hp", "word", "white"], ["word"], ["word", "hp_near"],
+                                     ["word", "hp"]][s])[0] for s in range(STREAMS_S)]
+    L = min(len(p) for p in pcms) // 1600 * 1600
+    return np.stack([p[:L] for p in pcms])
+
+
+def _oracle_shard(streams, audio, on_tick):
+    """Oracle level 1 + 2 over `streams`, tick by tick; on_tick(events, audio_by_key) per tick."""
+    from easywakeword_amd._lib import EVENT_DTYPE
+    from oracle import mfcc_ref
+    from oracle.gate_ref import DetectorRef, GateConfig
+    import synth
+    tm, ts = mfcc_ref.extract_mfcc(synth.load_word())
+    dets = [DetectorRef(GateConfig()) for _ in streams]
+    for t in range(audio.shape[1] // 1600):
+        rows, seg = [], {}
+        for j, (s, det) in enumerate(zip(streams, dets)):
+            ev = det.push_tick(audio[s, t * 1600:(t + 1) * 1600])
+            if ev is None:
+                continue
+            score = np.nan
+            if not ev.skipped:
+                cm, cs = mfcc_ref.extract_mfcc(ev.audio)
+                score = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
+            rows.append((j, ev.length, ev.tick, 0, ev.time, score, int(score >= 75.0), int(ev.skipped)))
+            seg[(j, ev.tick)] = ev.audio
+        on_tick(np.array(rows, dtype=EVENT_DTYPE), seg)
+
+
+def _worker_stream(rank, world, port, q):
+    _init(rank, world, port)
+    try:
+        from oracle.gate_ref import normalize_level3
+        audio = _stream_audio()
+        first, count = shard_streams(STREAMS_S, rank, world)
+        segs = {}
+
+        def audio_fn(ev):
+            return [torch.from_numpy(normalize_level3(segs[(int(e["stream"]), int(e["tick"]))])) for e in ev]
+
+        col = PositiveCollector(first, torch.device("cpu"), every=EVERY, audio_cap=10000, audio_fn=audio_fn)
+        got_rec, got_aud = [], []
+
+        def on_tick(ev, seg):
+            segs.update(seg)
+            col.add(ev)
+            rec, aud = col.tick()
+            if rec is not None:
+                got_rec.append(rec.numpy())
+                got_aud.extend(a.numpy() for a in aud)
+
+        _oracle_shard(range(first, first + count), audio, on_tick)
+        rec, aud = col.flush()
+        if rec is not None:
+            got_rec.append(rec.numpy())
+            got_aud.extend(a.numpy() for a in aud)
+        q.put((rank, (np.concatenate(got_rec), got_aud) if rank == 0 else (len(got_rec), len(got_aud))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_streaming_positives_reproduce_single_process(world):
+    """Sharded streaming (oracle gate + scorer per rank), positives gathered every 10
+    ticks with their level-3 PCM: rank 0 holds exactly the N=1 positives and audio."""
+    from oracle.gate_ref import normalize_level3
+    res = _run_world(_worker_stream, world)
+    rec, aud = res[0]
+    assert all(res[r] == (0, 0) for r in range(1, world))
+    audio = _stream_audio()
+    want, want_aud = [], {}
+
+    def on_tick(ev, seg):
+        for e in ev[(ev["match"] != 0) & ((ev["flags"] & 1) == 0)]:
+            key = (int(e["stream"]), int(e["tick"]))
+            want.append((key[0], key[1], int(e["length"]), int(np.float64(e["score"]).view(np.int64))))
+            want_aud[key] = normalize_level3(seg[key])
+
+    _oracle_shard(range(STREAMS_S), audio, on_tick)
+    n_ev_all = len(want)
+    assert n_ev_all >= 10
+    got = sorted(map(tuple, rec.tolist()))
+    assert got == sorted(want)
+    assert len(aud) == len(rec)
+    for r, a in zip(rec.tolist(), aud):
+        np.testing.assert_array_equal(a, want_aud[(r[0], r[1])])
