@@ -148,14 +148,30 @@ def _cpu_worker(args):
     return frames, n, time.perf_counter() - t0
 
 
+def host_cores():
+    """(processes to use, CPUs in this process's affinity mask, cgroup CPU quota in cores or None).
+    One process per usable core: the affinity count, capped by the cgroup CPU quota when one is
+    set (a GPU box's job may list 256 host CPUs but own 16 of them; more processes than the
+    quota would only time-share the same cores)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return max(1, min(aff, quota) if quota else aff), aff, quota
+
+
 def cpu_baseline(host_pcm, lengths, offsets, seconds):
     import multiprocessing as mp
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    procs = max(1, min(16, cores))
-    per = 400
+    procs, aff, quota = host_cores()
+    per = max(1, len(lengths) // procs)
     jobs = []
     for p in range(procs):
         idx = range(p * per, min(len(lengths), (p + 1) * per))
@@ -167,7 +183,8 @@ def cpu_baseline(host_pcm, lengths, offsets, seconds):
     frames = sum(r[0] for r in res)
     segs = sum(r[1] for r in res)
     wall = max(r[2] for r in res)
-    return {"value": frames / wall, "unit": "frames/s", "cores": procs, "kind": "port",
+    return {"value": frames / wall, "unit": "frames/s", "cores": procs, "host_cores_affinity": aff,
+            "cpu_quota_cores": quota, "kind": "port",
             "sample": f"{segs} segments ({frames} MFCC frames) of the same ragged batch, float64 candidate path, "
                       f"oracle/mfcc_ref.py (numpy/scipy restatement of librosa 0.11.0 mfcc + scipy cosine), "
                       f"{procs} processes x ~{seconds:.0f} s, OMP_NUM_THREADS=1"}
@@ -618,7 +635,7 @@ def main():
         out["fixed_length"] = fixed
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sample = min(n_seg, 16 * 400)
+        sample = min(n_seg, max(16, host_cores()[0]) * 400)
         host = pcm[: int(offsets[sample - 1] + lengths[sample - 1])].cpu().numpy()
         out["cpu_baseline"] = cpu_baseline(host, lengths[:sample], offsets[:sample], args.cpu_seconds)
         if not args.no_streaming:

@@ -10,7 +10,8 @@ MFCC + cosine matcher, as hand-written HIP kernels behind a C ABI
 from .engine import Engine, StreamEngine
 from .wakeword import SoundBuffer, WakeWord, WordMatcher
 from .audio import ArraySource, WavSource, load_wav, write_wav
+from .devices import AudioDeviceManager
 
 __all__ = ["WakeWord", "WordMatcher", "SoundBuffer", "Engine", "StreamEngine",
-           "ArraySource", "WavSource", "load_wav", "write_wav"]
+           "ArraySource", "WavSource", "load_wav", "write_wav", "AudioDeviceManager"]
 __version__ = "0.1.0"

@@ -40,7 +40,7 @@ EXPORTS = [
     "ewk_read_segment", "ewk_reset_streams", "ewk_set_similarity_threshold",
     "ewk_profile_enable", "ewk_profile_read",
     "ewk_push_pcm16", "ewk_push_many_pcm16", "ewk_normalize_segments", "ewk_normalize_events",
-    "ewk_decode_pcm16", "ewk_poll_lagged", "ewk_runtime_info",
+    "ewk_decode_pcm16", "ewk_poll_lagged", "ewk_runtime_info", "ewk_reenter",
 ]
 
 
@@ -135,6 +135,7 @@ def load():
             "ewk_read_last": (C.c_int, [_P, C.c_int32, C.c_int64, _fp, _i64p]),
             "ewk_read_segment": (C.c_int, [_P, C.c_int32, C.c_int64, C.c_int32, _fp]),
             "ewk_reset_streams": (C.c_int, [_P]),
+            "ewk_reenter": (C.c_int, [_P, C.c_int32, C.c_double]),
             "ewk_profile_enable": (C.c_int, [_P, C.c_int32]),
             "ewk_profile_read": (C.c_int, [_P, C.c_int32, _dp, _i64p]),
             "ewk_push_pcm16": (C.c_int, [_P, _P, C.c_int64, C.c_int32]),

@@ -96,8 +96,9 @@ class WavSource(ArraySource):
 
 
 class MicSource:
-    """PortAudio microphone through ``sounddevice`` (only when installed; the
-    host device picking of AudioDeviceManager is out of scope)."""
+    """PortAudio microphone through ``sounddevice`` (only when installed); `device` is a
+    PortAudio index -- easywakeword_amd.devices.AudioDeviceManager resolves names and
+    the reference's magic words."""
 
     realtime = True
 

@@ -1107,6 +1107,19 @@ int ewk_poll_lagged(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out) 
     return rc;
 }
 
+int ewk_reenter(ewk_engine* e, int32_t stream, double reentry_timeout) {
+    if (!e) return fail(EWK_EINVAL, "engine is NULL");
+    if (e->n_streams <= 0) return fail(EWK_EINVAL, "engine has no streams");
+    if (stream < -1 || stream >= e->n_streams) return fail(EWK_EINVAL, "stream index out of range");
+    if (!(reentry_timeout == reentry_timeout)) return fail(EWK_EINVAL, "reentry_timeout is NaN");
+    HIP_TRY(hipSetDevice(e->device));
+    e->cfg.reentry_timeout = reentry_timeout;   // read by every later gate launch
+    const int32_t first = stream < 0 ? 0 : stream;
+    const int32_t n = stream < 0 ? e->n_streams : 1;
+    HIP_TRY(launch_reenter(e->d_st, first, n, e->cfg.tick_seconds, e->stream));
+    return EWK_OK;
+}
+
 int ewk_get_stream_state(ewk_engine* e, int32_t stream, ewk_stream_state* out) {
     if (!e || !out) return fail(EWK_EINVAL, "NULL argument");
     if (stream < 0 || stream >= e->n_streams) return fail(EWK_EINVAL, "stream index out of range");

@@ -89,6 +89,7 @@ struct GateArgs {
 };
 
 hipError_t launch_gate(const GateArgs& g, hipStream_t s);
+hipError_t launch_reenter(GateStream* st, int32_t first, int32_t n, double tick_seconds, hipStream_t s);
 // register-resident block RMS arrays up to 64 * kGateRegMax blocks (10 s ring: block >= 313 samples)
 constexpr int kGateRegMax = 8;
 int gate_val_len(const PwTree* trees_host, int n_blocks);

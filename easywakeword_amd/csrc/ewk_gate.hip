@@ -792,6 +792,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
 #endif
 }
 
+// _detect_word entry (wakeword.py:1048-1057) for streams whose detection runs: state from
+// the current is_silent(), start_time = now.  Streams still filling their ring are left
+// alone (their entry happens in k_gate_ticks when the ring first fills).
+__global__ void k_reenter(GateStream* st, int32_t first, int32_t n, double tick_seconds) {
+    const int i = first + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= first + n) return;
+    GateStream s = st[i];
+    if (!s.started) return;
+    const double now = (double)s.tick * tick_seconds;
+    s.state = s.last_silent ? kInSilence : kWaiting;
+    if (s.last_silent) s.silence_start = now;
+    s.start_time = now;
+    st[i] = s;
+}
+
+hipError_t launch_reenter(GateStream* st, int32_t first, int32_t n, double tick_seconds, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_reenter, dim3((n + 255) / 256), dim3(256), 0, s, st, first, n, tick_seconds);
+    return hipGetLastError();
+}
+
 int gate_val_len(const PwTree* trees_host, int n_blocks) {
     int m = 0;
     for (int k = 0; k < kNumTrees; ++k) m = std::max(m, 10 * trees_host[k].n_leaves);

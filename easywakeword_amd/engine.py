@@ -293,3 +293,9 @@ class StreamEngine(Engine):
 
     def reset(self) -> None:
         check(self._lib.ewk_reset_streams(self._h))
+
+    def reenter(self, stream: int = -1, reentry_timeout: float = 0.0) -> None:
+        """A new _detect_word call (wakeword.py:1048-1057) on `stream` (-1 = all) and the
+        re-entry timeout for later pushes (0 = continuous, > 0 = start() mode)."""
+        check(self._lib.ewk_reenter(self._h, int(stream), float(reentry_timeout)))
+        self.config.reentry_timeout = float(reentry_timeout)

@@ -171,8 +171,13 @@ class SoundBuffer:
 
 
 def _default_source(device):
+    """The microphone `device` names (None, index, name pattern, "default"/"best"/"first"),
+    resolved like the reference's AudioDeviceManager.select_device (wakeword.py:128-185,
+    437); an unmatched spec raises ValueError instead of falling back to the default mic."""
+    from .devices import AudioDeviceManager
     try:
-        return _audio.MicSource(device=device if isinstance(device, int) else None, block=BLOCK)
+        index = AudioDeviceManager.select_device(device)
+        return _audio.MicSource(device=index, block=BLOCK)
     except (ImportError, OSError) as exc:
         raise OSError("no audio input available (sounddevice/PortAudio missing); "
                       "pass source=ArraySource(...) or WavSource(...)") from exc
@@ -381,14 +386,22 @@ class WakeWord:
                     reentry_timeout=float(self.timeout) if reentry else 0.0)
 
     def _initialize_audio(self, reentry: bool = False) -> None:
+        """Buffer + matcher on first use; every call is a new _detect_word entry
+        (wakeword.py:1048-1057) in the mode of its caller: waitforit() continuous,
+        start() with the re-entry timeout."""
         if self._sound_buffer is None:
             src = self._source if self._source is not None else _default_source(self.device)
             self._sound_buffer = SoundBuffer(self.buffer_seconds, source=src, gpu=self._gpu,
                                              **{k: v for k, v in self._gate_config(reentry).items()
                                                 if k not in ("buffer_seconds", "block")})
+        else:
+            self._sound_buffer.engine.reenter(0, float(self.timeout) if reentry else 0.0)
         if self._matcher is None:
-            self._matcher = WordMatcher(sample_rate=FREQUENCY, engine=self._sound_buffer.engine)
+            # its own scorer engine: matches(threshold=...) must not move the stream's threshold
+            self._matcher = WordMatcher(sample_rate=FREQUENCY, gpu=self._gpu)
             self._matcher.load_reference_from_file(self.wavword, self.textword)
+            self._sound_buffer.engine.set_template(self._matcher.reference_mfcc_mean,
+                                                   self._matcher.reference_mfcc_std)
 
     def _wait_for_buffer(self) -> None:
         while not self._sound_buffer.is_buffer_full():
@@ -474,13 +487,11 @@ class WakeWord:
                 self._wait_for_buffer()
                 eng = self._sound_buffer.engine
                 while not self._stop_event.is_set():
-                    if self._sound_buffer.source.exhausted and not getattr(self._sound_buffer.source, "realtime", False):
-                        # a finite source has ended: keep feeding silence like an idle microphone
-                        pass
-                    self._sound_buffer.pump()
+                    self._sound_buffer.pump()   # a finite source keeps feeding silence, like an idle mic
                     res = self._handle_events(eng.poll())
                     if res and self.callback:
                         self.callback(res)
+                        eng.reenter(0, float(self.timeout))   # _detect_word returned: the loop calls it again
             finally:
                 self._listening = False
 

@@ -193,6 +193,11 @@ int ewk_poll(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out);
  * keeps working on tick t while the host consumes tick t-1 (one call of latency). */
 int ewk_poll_lagged(ewk_engine* e, ewk_event* out, int32_t cap, int32_t* n_out);
 int ewk_get_stream_state(ewk_engine* e, int32_t stream, ewk_stream_state* out);
+/* A new WakeWord._detect_word call (wakeword.py:1048-1057) on `stream` (-1 = all): for
+ * streams whose detection runs, the FSM restarts from the current is_silent() with
+ * start_time = now; `reentry_timeout` (<= 0: continuous, > 0: start()-mode re-entry
+ * every reentry_timeout s) applies to every later push.  Stream-ordered, asynchronous. */
+int ewk_reenter(ewk_engine* e, int32_t stream, double reentry_timeout);
 /* SoundBuffer.return_last_n_seconds(n) (wakeword.py:498-513) as float32 (ring values are the float32 input). */
 int ewk_read_last(ewk_engine* e, int32_t stream, int64_t n_samples, float* out, int64_t* n_out);
 /* Copy the samples of a queued/polled event (ring must not have wrapped over it). */
