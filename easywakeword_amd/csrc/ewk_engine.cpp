@@ -741,7 +741,7 @@ static int score_pending(ewk_engine* e, hipStream_t ss, const int32_t* n_events)
     a.rescore_count = e->d_work + 2;
     {
         ProfScope ps(e, 0, ss);
-        HIP_TRY(launch_score_f32(e->d_tab, a, 1, ss));
+        HIP_TRY(launch_score_f32(e->d_tab, a, e->n_streams >= kRingWaveStreams ? 2 : 1, ss));
     }
     const int64_t per = (1 + e->sring_len / HOP) * (NMEL + NMFCC);
     {

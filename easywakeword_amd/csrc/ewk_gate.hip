@@ -36,29 +36,7 @@
 // float64 parity with numpy requires un-fused multiply/add (e.g. the percentile lerp)
 #pragma clang fp contract(off)
 
-#ifndef EWK_GATE_NT
-#define EWK_GATE_NT 1   // 1: non-temporal tick loads (read once; measured -6%), 2: also non-temporal ring stores (no gain)
-#endif
-#ifndef EWK_GATE_ABLATE
-#define EWK_GATE_ABLATE 0   // timing-only ablations (scripts/mb_gate.py): 1 no a2, 2 no ring stores, 4 no tick loads
-#endif
-#ifndef EWK_GATE_GRID_MAX
-#define EWK_GATE_GRID_MAX 1024   // workgroups of 4 waves: 256 CUs x 16 waves (4 waves/SIMD)
-#endif
-#ifndef EWK_GATE_TIMING
-#define EWK_GATE_TIMING 0   // per-phase s_memtime accounting (scripts/mb_gate.py variants only)
-#endif
-
 namespace ewk {
-
-#if EWK_GATE_TIMING
-__device__ unsigned long long g_gtim[16];
-#define GT_TS(x) const uint64_t x = __builtin_amdgcn_s_memtime()
-#define GT_ACC(i, a, b) (gt[i] += (b) - (a))
-#else
-#define GT_TS(x)
-#define GT_ACC(i, a, b)
-#endif
 
 // ---- host: flatten numpy's pairwise recursion for one chunk --------------------
 static int split_point(int n) {
@@ -270,12 +248,10 @@ __device__ __forceinline__ double percentile25_sorted(const double* sorted, int 
     return r;
 }
 
-#ifndef EWK_GATE_DMA
-#define EWK_GATE_DMA 2   // float32 tick ingest by LDS-DMA (0: register chunks, 1: 4-B pieces, 2: 16-B pieces when aligned)
-#endif
-#ifndef EWK_GATE_WPE
-#define EWK_GATE_WPE 4   // min waves per SIMD the register allocator must allow (121 VGPRs; 5 spills and runs 37 % slower)
-#endif
+// the register allocator must allow 4 waves per SIMD (121 VGPRs; 5 spill and run 37 % slower)
+constexpr int kGateWavesPerEU = 4;
+// workgroups of 4 waves: 256 CUs x 16 waves (4 per SIMD); more streams loop inside the waves
+constexpr int kGateGridMax = 1024;
 constexpr int kDma4Chunks = 8;     // 16-B DMA path: ticks of up to 8 * 256 samples copied to the ring in one batch
 constexpr int kIngestLoads = 4;    // tick samples per lane loaded ahead of the ring stores (16: 166 VGPRs, 3 waves/SIMD, 10 % slower)
 
@@ -390,7 +366,7 @@ __device__ __forceinline__ double reg_percentile25(const double (&so)[RB], int n
 // wave shuffles, stored once -- no dependent global round trips per tick.  RB = 0:
 // both stay in global memory (any n_blocks).
 template <int RB, int DMA>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WPE, 8))) void k_gate_ticks(GateArgs g) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesPerEU, 8))) void k_gate_ticks(GateArgs g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const PwTree* __restrict__ trees = g.trees;   // read-only, cache-resident
@@ -417,12 +393,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
 #pragma unroll
         for (int m = 0; m < kIngestLoads; ++m) {
             const int i = c0 + lane + 64 * m;
-#if EWK_GATE_NT
             xin[m] = i < fs ? (g.pcm16 ? (float)__builtin_nontemporal_load(g.pcm16 + so + i) * (1.0f / 32768.0f)
                                        : __builtin_nontemporal_load(g.pcm + so + i)) : 0.0f;
-#else
-            xin[m] = i < fs ? (g.pcm16 ? (float)g.pcm16[so + i] * (1.0f / 32768.0f) : g.pcm[so + i]) : 0.0f;
-#endif
         }
     };
     // float32 input with the tick staged in LDS: the tick's samples go global -> LDS by
@@ -433,7 +405,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
     auto dma_tick = [&](int ss, int t) {
         const float* src = g.pcm + (int64_t)ss * g.stride + (int64_t)t * g.tick_stride;
         if (DMA == 2) {   // 16-B pieces (1 KiB per wave-instruction): tick rows 16-B aligned, block % 4 == 0
-            for (int c0 = 0; c0 < ((EWK_GATE_ABLATE & 4) ? 0 : fs); c0 += 256) {
+            for (int c0 = 0; c0 < fs; c0 += 256) {
                 if (c0 + 4 * lane < fs)
                     __builtin_amdgcn_global_load_lds(src + c0 + 4 * lane,
                                                      (__attribute__((address_space(3))) void*)(stage + c0), 16, 0, 0);
@@ -457,10 +429,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
     const PwTree* tbr = trees + kTreeBlockRem;
     const PwTree* tlf = trees + kTreeLastFull;
     const PwTree* tlr = trees + kTreeLastRem;
-#if EWK_GATE_TIMING
-    uint64_t gt[8] = {};
-#endif
-    GT_TS(q_begin);
     constexpr int RBn = RB > 0 ? RB : 1;
     double gr[RBn], srt[RBn];
     if (RB > 0) {   // (this path never double-buffers: sorted_sel stays 0)
@@ -472,10 +440,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
         }
     }
 
-    GT_TS(q_loaded);
-    GT_ACC(0, q_begin, q_loaded);
     for (int t = 0; t < g.n_ticks; ++t) {
-        GT_TS(q0);
         const int64_t tick = g.tick0 + t + 1;                    // tick being delivered
         const double t_prev = (double)(tick - 1) * g.tick_seconds;
         // start()-mode re-entry (TimeoutError -> _detect_word again), before the sleep
@@ -505,7 +470,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     const int i = 256 * (h + c) + 4 * lane;
-                    if (i < fs && !(EWK_GATE_ABLATE & 2)) {
+                    if (i < fs) {
                         int k = sp0 + i;
                         if (k >= Rs) k -= Rs;
                         *reinterpret_cast<float4*>(ring + k) = xv[c];
@@ -541,11 +506,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
                 if (i < fs) {
                     int k = sp0 + i;
                     if (k >= Rs) k -= Rs;
-#if EWK_GATE_NT & 2
-                    __builtin_nontemporal_store(xin[m], ring + k);
-#else
                     ring[k] = xin[m];
-#endif
                     if (staged) stage[i] = xin[m];
                 }
             }
@@ -558,13 +519,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
         st.spos = (int32_t)((sp0 + fs) % Rs);
         st.collected = min(st.collected + (int64_t)fs, (int64_t)R);
         const bool full = st.collected >= R;
-        GT_TS(q1);
-        GT_ACC(1, q0, q1);
         // block sum of the window when it coincides with a refreshed block
         double reuse_sum = 0.0;
         bool have_reuse = false;
         // ---- a2: threshold over the physical blocks (only once the ring is full)
-        if (full && !(EWK_GATE_ABLATE & 1)) {
+        if (full) {
             auto block_sum = [&](int b) -> double {
                 const int a0 = b * fs;
                 if (staged && a0 == p0)   // the block is exactly this tick's samples
@@ -651,7 +610,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
             const double thr = p25 * 1.5;
             // Python max(new, MIN): MIN only if MIN > new
             st.threshold = (g.min_threshold > thr) ? g.min_threshold : thr;
-        } else if (g.compact && !(EWK_GATE_ABLATE & 1)) {
+        } else if (g.compact) {
             // filling a compact ring: keep this block's RMS now (its samples will not all
             // be in the sample ring when the reference ring first fills)
             const int b = p0 / fs;
@@ -660,8 +619,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
             if (RB > 0) reg_set(gr, b, v, lane);
             else if (lane == 0) grms[b] = v;
         }
-        GT_TS(q2);
-        GT_ACC(2, q1, q2);
         // ---- a3: is_silent(): RMS of the last n_last samples < threshold
         bool silent = true;
         if (nl > 0) {
@@ -691,8 +648,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             dma_tick(s + wstride, 0);
         }
-        GT_TS(q3);
-        GT_ACC(3, q2, q3);
         st.last_silent = silent;
         st.tick = tick;
         const double now = (double)tick * g.tick_seconds;
@@ -767,8 +722,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
         st.sound_start = __shfl(st.sound_start, 0, 64);
         st.sound_end = __shfl(st.sound_end, 0, 64);
     }
-    GT_TS(q_loop);
-    GT_ACC(4, q_loaded, q_loop);
     if (RB > 0 && (st.filled || g.compact)) {
 #pragma unroll
         for (int j = 0; j < RBn; ++j) {
@@ -781,15 +734,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EWK_GATE_WP
     if (s >= g.n_streams) break;
     if (!dma) load_chunk(0, 0);
     }
-#if EWK_GATE_TIMING
-    GT_TS(q_end);
-    GT_ACC(5, q_loop, q_end);
-    GT_ACC(6, q_begin, q_end);
-    if (lane == 0) {
-        for (int i = 0; i < 7; ++i) atomicAdd(&g_gtim[i], (unsigned long long)gt[i]);
-        atomicAdd(&g_gtim[7], 1ull);
-    }
-#endif
 }
 
 // _detect_word entry (wakeword.py:1048-1057) for streams whose detection runs: state from
@@ -824,13 +768,13 @@ hipError_t launch_gate(const GateArgs& g, hipStream_t s) {
     if (g.n_streams <= 0 || g.n_ticks <= 0) return hipSuccess;
     // at most one resident wave per stream slot (16 waves/CU at 4 waves/SIMD); more
     // streams loop inside the waves
-    const int grid = std::min((g.n_streams + 3) / 4, EWK_GATE_GRID_MAX);
+    const int grid = std::min((g.n_streams + 3) / 4, kGateGridMax);
     const size_t per_wave = (size_t)g.val_len * 8 + (size_t)g.stage * 4;
     const size_t lds = 4 * per_wave;
     const int64_t nl = std::min<int64_t>(g.n_last, g.ring_len);
-    const bool dma = EWK_GATE_DMA && g.pcm16 == nullptr && g.stage >= g.block && g.stage >= nl;
+    const bool dma = g.pcm16 == nullptr && g.stage >= g.block && g.stage >= nl;
     // 16-B pieces: every tick row 16-B aligned, whole 4-sample groups that never straddle the ring wrap
-    const bool dma4 = dma && EWK_GATE_DMA >= 2 && g.block % 4 == 0 && g.block <= 256 * kDma4Chunks &&
+    const bool dma4 = dma && g.block % 4 == 0 && g.block <= 256 * kDma4Chunks &&
                       g.stride % 4 == 0 && g.tick_stride % 4 == 0 && g.ring_len % 4 == 0 && g.sring_len % 4 == 0 &&
                       ((uintptr_t)g.pcm & 15) == 0;
     if (g.n_blocks <= 128) {
@@ -849,10 +793,3 @@ hipError_t launch_gate(const GateArgs& g, hipStream_t s) {
 
 }  // namespace ewk
 
-#if EWK_GATE_TIMING
-extern "C" int ewk_debug_gate_timing(unsigned long long* out) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ewk::g_gtim), 16 * sizeof(unsigned long long)) != hipSuccess) return -3;
-    unsigned long long z[16] = {};
-    return hipMemcpyToSymbol(HIP_SYMBOL(ewk::g_gtim), z, sizeof(z)) == hipSuccess ? 0 : -3;
-}
-#endif

@@ -18,22 +18,11 @@ constexpr int NMEL = 128;
 constexpr int NMFCC = EWK_N_MFCC;    // 20
 constexpr int MEL_ITERS = 40;        // unrolled mel FMAs per lane: sum of per-group band widths
 constexpr int SCR_FRAME = 272;       // per-frame FFT scratch floats (16 rows x 17)
-// fp32 scorer shape: frames per 16-lane group per pass (kNF), waves per workgroup and
-// workgroups per CU.  kNF = 2 doubles the per-wave FFT state (ILP) and its LDS, so the
-// CU holds one 8-wave workgroup instead of two 4-wave ones (same 2 waves per SIMD).
-#ifndef EWK_NF
-#define EWK_NF 2
-#endif
-constexpr int kNF = EWK_NF;
-// kNF = 2: the untangle pairs conjugate bins inside a lane (two columns of one frame)
-#ifndef EWK_PAIR
-#define EWK_PAIR (EWK_NF == 2)
-#endif
-#ifndef EWK_WAVES
-#define EWK_WAVES (EWK_NF == 1 ? 4 : 8)   // timing probes may shrink it (waves per SIMD)
-#endif
-constexpr int WAVES = EWK_WAVES;
-constexpr int kScoreWGsPerCU = kNF == 1 ? 2 : 1;
+// fp32 scorer shape: two frames per 16-lane group per pass (kNF, two independent FFT
+// instruction streams per lane; the untangle pairs conjugate bins inside a lane), eight
+// waves per workgroup, one workgroup per CU (2 waves per SIMD at 256 VGPRs).
+constexpr int kNF = 2;
+constexpr int WAVES = 8;
 
 // Host-built constant tables (ewk_tables.cpp); copied to LDS by every workgroup.
 struct Tables {
@@ -100,14 +89,18 @@ struct ScoreArgs {
     int32_t* adv_ev_base;
 };
 
+// ring_mode: 0 linear batch, 1 ring events one segment per workgroup, 2 ring events one
+// segment per wave (many events per tick)
 hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mode, hipStream_t s);
+// streams from which a tick's events are scored one segment per wave (ring_mode 2)
+constexpr int kRingWaveStreams = 65536;
 // ScoreArgs::order holds n_seg indices followed by kLptScratch ints of bucket counters
 constexpr int kLptScratch = 128;
 // ring mode: *ev_base = *n_events after a scoring pass; zero the ring-mode work counter and re-score count
 hipError_t launch_snapshot(const int32_t* src, int32_t* dst, hipStream_t s);   // *dst = *src, stream-ordered
 hipError_t launch_advance_watermark(int32_t* ev_base, const int32_t* n_events, int32_t* work,
                                     int32_t* rescore_count, hipStream_t s);
-constexpr int kScoreGridMax = 256 * kScoreWGsPerCU;   // one resident workgroup wave of the grid
+constexpr int kScoreGridMax = 256;   // one resident workgroup wave of the grid
 constexpr int kScoreGridRing = 256;                     // ring-mode grid (device-side event count)
 int score_grid(int n_seg, int ring_mode);
 // log-mel tiles parked per wave for the top_db pass: segments up to 3 s (T <= 301)

@@ -6,65 +6,52 @@
 // feature.mfcc(n_mfcc=20, n_fft=512, hop=160) + scipy cosine + the score
 // scaling, for many segments per launch.
 //
-// Design (one wave = one segment; 4 waves per workgroup share the tables;
-// a persistent grid pulls segments from an atomic work counter):
+// Design.  Linear batches: one wave = one segment; a persistent grid (one 8-wave
+// workgroup per CU sharing the LDS tables) pulls segments from an atomic work counter in
+// longest-first order.  Ring events of a streaming tick: one segment per workgroup (its
+// tiles spread over the 8 waves) for a few hundred events, one per wave for many.
 //   frames  : stft(center=True, pad_mode=constant): frame t covers samples
 //             [t*160-256, t*160+256) of the segment, zero outside; T = 1+L//160.
-//   staging : the 4 frames of a wave pass span 992 contiguous samples; they are
-//             loaded one pass ahead with coalesced dword loads (bounds / ring wrap
-//             resolved once per sample) and parked in LDS.
-//   FFT     : 16 lanes per frame, 4 frames per wave pass.  The 512-point real
-//             frame is packed as 256 complex points z[n] = x[2n] + i x[2n+1];
-//             256 = 16 x 16 four-step FFT: a register DFT16 per lane, a
-//             twiddle, an LDS transpose, a second register DFT16, then the
-//             real-FFT untangle X[k] = (Z[k]+Z*[256-k])/2 - i W512^k (Z[k]-Z*[256-k])/2.
-//   mel     : Slaney bands from LDS, fully unrolled with compile-time group
-//             widths (band m = j + 16 i; widths {2,2,2,3,4,6,9,12} cover every
-//             band, weights zero-padded), then 10*log10(max(1e-10, .)) via
-//             v_log_f32; written to a 16-frame log-mel tile.
+//             Samples come through a buffer descriptor whose range check returns 0
+//             outside the segment (the padding); ring segments wrap at the stream ring.
+//   staging : a wave pass is 8 frames spanning 1,632 contiguous samples, loaded one
+//             pass ahead with coalesced dword loads and stored to LDS with
+//             ds_write_addtid_b32.
+//   FFT     : 16 lanes per frame, two frames per 16-lane group (8 frames per pass: two
+//             independent instruction streams per lane).  The 512-point real frame is
+//             packed as 256 complex points z[n] = x[2n] + i x[2n+1]; 256 = 16 x 16
+//             four-step FFT: a register DFT16 (window folded into its first stage,
+//             tan-factored W16 twiddles), a twiddle, an LDS transpose, a second DFT16,
+//             then the real-FFT untangle with each bin and its conjugate partner in the
+//             same lane (no cross-lane traffic).
+//   mel     : Slaney bands from LDS, fully unrolled with compile-time group widths
+//             (band m = j + 16 i; widths {2,2,2,3,4,6,9,12}, weights zero-padded), then
+//             10*log10(max(1e-10, .)) via v_log_f32; written to a 16-frame log-mel tile
+//             as f16 hi/lo pairs (hi = x truncated to 11 bits, lo = x - hi).
 //   DCT     : the only dense GEMM on the path: C[32 x 16] = D[32 x 128] . X[128 x 16]
-//             per 16-frame tile on the matrix cores (v_mfma_f32_16x16x4_f32, exact
-//             f32 fma chains), rows 20..31 zero.
-//   top_db  : power_to_db clamps at (segment max - 80 dB), a segment-global
-//             coupling.  Pass 1 computes the unclamped DCT, tracks the log-mel
-//             max/min and parks every log-mel tile in a per-wave global scratch;
-//             if min < max-80, pass 2 re-reads the tiles, clamps and redoes only
-//             the DCT + statistics (no FFT).
+//             per 16-frame tile on the matrix cores, v_mfma_f32_16x16x32_f16 on the hi/lo
+//             splits (Dh Xh + Dh Xl + Dl Xh, f32 accumulation), rows 20..31 zero.
+//   top_db  : power_to_db clamps at (segment max - 80 dB), a segment-global coupling.
+//             Pass 1 clamps each tile speculatively at the running max - 80 dB (exact
+//             once the max is known), parks the stored tile + its DCT columns in a
+//             per-wave global scratch and records the tile minimum; if the segment
+//             min is below the final max - 80 dB, pass 2 revisits only the tiles whose
+//             stored minimum is below it, clamps and swaps their contribution in the
+//             statistics (no second FFT).
 //   stats   : population mean/std over frames from fp64 shifted sums
 //             (d = c - c[frame 0]) -- exact 0 std for identical frames.
 //   score   : the reference's own float32 / float64 cosine arithmetic
-//             (wakeword.py:611-625 + scipy correlation); NaN kept.
+//             (wakeword.py:611-625 + scipy correlation); NaN kept.  Near-threshold
+//             scores are re-scored by k_score_f64 (fp64 path, below).
 #include <hip/hip_runtime.h>
 #include <math.h>
 
 #include "ewk_internal.h"
 
-#ifndef EWK_ABLATE
-#define EWK_ABLATE 0   // timing-only ablations (scripts/mb_score.py); 0 in every real build
-#endif
-
-#ifndef EWK_ADDTID_STAGE
-#define EWK_ADDTID_STAGE 1   // sample staging with ds_write_addtid_b32 (0: ds_write_b32)
-#endif
-
-#ifndef EWK_PRIO
-#define EWK_PRIO 2   // s_setprio 1 over the frame-pass LDS phases (window, transposes, mel): -0.4 %; 1 = VALU phases high: +1 %
-#endif
+// s_setprio 1 over the frame-pass LDS phases (window, transposes, mel): -0.4 %
 #define EWK_SETPRIO(v) __builtin_amdgcn_s_setprio(v)
-#ifndef EWK_TIMING
-#define EWK_TIMING 0   // per-phase s_memtime accounting (scripts/mb_score.py variants only)
-#endif
 
 namespace ewk {
-
-#if EWK_TIMING
-__device__ unsigned long long g_tim[24];
-#define EWK_TS(x) const uint64_t x = __builtin_amdgcn_s_memtime()
-#define EWK_TACC(i, a, b) (tim[i] += (b) - (a))
-#else
-#define EWK_TS(x)
-#define EWK_TACC(i, a, b)
-#endif
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
@@ -81,10 +68,7 @@ constexpr int kScrFrames = kFPP * SCR_FRAME + 8 * (kNF - 1);
 // so the second frame's first 11 sample pairs are the first frame's pairs 5..15 (hop 160 =
 // 5 x 32) and only 5 more are read.  The stage is skewed -- sample s at s + 32 floor(s / 320)
 // -- so the four lane groups' frames (320 samples apart) land 32 banks apart.
-#ifndef EWK_FPAIR
-#define EWK_FPAIR (EWK_NF == 2)
-#endif
-__host__ __device__ constexpr int stg_off(int c) { return 256 * c + (EWK_FPAIR ? 128 * (c / 5) : 0); }   // bytes of stage row c
+__host__ __device__ constexpr int stg_off(int c) { return 256 * c + 128 * (c / 5); }   // bytes of stage row c
 __host__ __device__ constexpr int win_off(int g, int n1) {   // bytes: pair n1 of slot g from the lane's base
     return 4 * (160 * g + 32 * n1 + 32 * ((160 * g + 32 * n1) / 320));
 }
@@ -125,7 +109,7 @@ constexpr int W_BYTES = W_TMIN + ((kLmTiles * 4 + 15) & ~15);
 constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
 constexpr int LDS_BYTES = L_WG + 16 + 8 * WAVES;
 constexpr int kRescoreFrames = 16;
-static_assert(LDS_BYTES * kScoreWGsPerCU <= 160 * 1024, "the workgroups of a CU must fit its LDS");
+static_assert(LDS_BYTES <= 160 * 1024, "the workgroup must fit a CU's LDS");
 static_assert(16 % kFPP == 0, "passes must tile the 16-frame log-mel tile");
 
 
@@ -307,7 +291,6 @@ __device__ __forceinline__ void clamp_store(float* tile, int lane, const uint4 (
     }
 }
 
-#if EWK_PAIR
 // FFT transpose image of one pass (one real or imaginary plane): row k1 of frame set g
 // holds the 64 lanes' values (16 f + j) contiguously, as ds_write_addtid_b32 stores them
 // (address = M0 + offset + 4 lane).  Rows are placed so that the untangle's row reads
@@ -319,7 +302,6 @@ __host__ __device__ constexpr int tr_off(int r, int h) {
     const int q = (jp >> 2) + (r >= 8 ? 2 : 0);
     return 64 * (16 * h + 4 * (jp & 3) + q) + 4 * ((jp & 3) + 8 * h);   // floats
 }
-#endif
 
 // Segment samples through a buffer descriptor: the hardware range check returns 0
 // outside [0, len) (negative offsets wrap to huge unsigned ones), which is exactly
@@ -356,9 +338,6 @@ __device__ __forceinline__ void stage_load(const SegSrc<RING>& v, int q0, int la
 #pragma unroll
     for (int c = 0; c < kStageLoads; ++c) {
         const int q = q0 + 64 * c + lane;
-#if EWK_ABLATE & 1
-        r[c] = ((unsigned)q < (unsigned)v.len) ? (float)((q * 7) & 255) * 1e-3f : 0.0f;
-#else
         int off;
         if (RING) {
             const int phys = q >= v.wrap_at ? q - v.wrap_at : q + v.start;
@@ -367,11 +346,9 @@ __device__ __forceinline__ void stage_load(const SegSrc<RING>& v, int q0, int la
             off = q * 4;
         }
         r[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(v.rsrc, off, 0, 0));
-#endif
     }
 }
 
-#if EWK_PAIR
 // 13 lane-contiguous rows of 64 floats with ds_write_addtid_b32 (M0 = stage base, saved
 // and restored; s_nop 0 for the M0 -> LDS hazard): half the LDS cycles of ds_write_b32
 #define EWK_ST13(o)                                                                                            \
@@ -394,17 +371,11 @@ __device__ __forceinline__ void stage_load(const SegSrc<RING>& v, int q0, int la
                    [o12] "i"(stg_off(o + 12))                                                                     \
                  : "memory")
 static_assert(kStageLoads == 26, "stage_store writes two blocks of 13 rows");
-#endif
 __device__ __forceinline__ void stage_store(float* stage, int lane, const float (&r)[kStageLoads]) {
-#if EWK_PAIR && EWK_ADDTID_STAGE
     const uint32_t m0base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)stage);
     uint32_t m0save;
     EWK_ST13(0);
     EWK_ST13(13);
-#else
-#pragma unroll
-    for (int c = 0; c < kStageLoads; ++c) stage[stg_off(c) / 4 + lane] = r[c];
-#endif
 }
 
 constexpr int kMelW[8] = {2, 2, 2, 3, 4, 6, 9, 12};   // per 16-band group (checked on the host)
@@ -424,26 +395,21 @@ template <int RING>
 __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T, int row0, bool next,
                                            const unsigned char* smem, float* scr, float* tile,
                                            int lane, const int (&lo)[8], float& vmax, float& vmin,
-                                           float clampv = -INFINITY, uint64_t* tim = nullptr) {
-#if EWK_PRIO == 2
+                                           float clampv = -INFINITY) {
     EWK_SETPRIO(1);
-#endif
-    EWK_TS(p0);
     // lane group f = lane>>4 holds frames fr = 4 g + f (g < kNF) of this pass; the
     // kNF frames of a lane are independent instruction streams (ILP for the wave).
     const int f = lane >> 4, j = lane & 15;
-#if EWK_PAIR
     // after the transpose lane (h, j') = (j >> 3, j & 7) owns bin columns rowA = j' and
     // rowB = 16 - j' (8 for j' = 0) of frame 4h + f (scratch scf)
     const int jp = j & 7;
     const int rowA = jp, rowB = jp ? 16 - jp : 8;
     float* scf = scr + (4 * (j >> 3) + f) * SCR_FRAME + 8 * (j >> 3);
-#endif
     bool valid[kNF];
     float* sc[kNF];
 #pragma unroll
     for (int g = 0; g < kNF; ++g) {
-        valid[g] = t0 + (EWK_FPAIR ? 2 * f + g : 4 * g + f) < T;
+        valid[g] = t0 + 2 * f + g < T;
         sc[g] = scr + (4 * g + f) * SCR_FRAME + 8 * g;
     }
 
@@ -454,7 +420,6 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     floatx4 t4[8];   // twiddle row W256^(j*k1)
     {
         float2 x[kNF][16];
-#if EWK_FPAIR
         {
             const uint32_t sa = (uint32_t)(uintptr_t)(scr + 352 * f + 2 * j);
 #define EWK_LD64(g, n) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(x[g][n]) : "v"(sa), "i"(win_off(g, n)) : "memory")
@@ -464,20 +429,9 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
             EWK_LD64(1, 11); EWK_LD64(1, 12); EWK_LD64(1, 13); EWK_LD64(1, 14); EWK_LD64(1, 15);
 #undef EWK_LD64
         }
-#else
-#pragma unroll
-        for (int g = 0; g < kNF; ++g) {
-            const uint32_t sa = (uint32_t)(uintptr_t)(scr + (4 * g + f) * HOP + 2 * j);
-#define EWK_LD64(n) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(x[g][n]) : "v"(sa), "i"(128 * (n)) : "memory")
-            EWK_LD64(0); EWK_LD64(1); EWK_LD64(2); EWK_LD64(3); EWK_LD64(4); EWK_LD64(5); EWK_LD64(6); EWK_LD64(7);
-            EWK_LD64(8); EWK_LD64(9); EWK_LD64(10); EWK_LD64(11); EWK_LD64(12); EWK_LD64(13); EWK_LD64(14); EWK_LD64(15);
-#undef EWK_LD64
-        }
-#endif
         floatx4 w4[8];   // this lane's window pairs, fetched in the same batch
         EWK_LD128_8(w4, (uint32_t)(uintptr_t)(reinterpret_cast<const float4*>(smem + L_WIN2) + j * (TP / 2)));
         EWK_WAIT_8(w4);
-#if EWK_FPAIR
         asm volatile("s_waitcnt lgkmcnt(0)"
                      : "+v"(x[0][0]), "+v"(x[0][1]), "+v"(x[0][2]), "+v"(x[0][3]), "+v"(x[0][4]), "+v"(x[0][5]),
                        "+v"(x[0][6]), "+v"(x[0][7]), "+v"(x[0][8]), "+v"(x[0][9]), "+v"(x[0][10]), "+v"(x[0][11]),
@@ -490,27 +444,13 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
                      : "memory");
 #pragma unroll
         for (int n = 0; n <= 10; ++n) x[1][n] = x[0][n + 5];   // the shared sample pairs
-#else
-#pragma unroll
-        for (int g = 0; g < kNF; ++g)
-            asm volatile("s_waitcnt lgkmcnt(0)"
-                         : "+v"(x[g][0]), "+v"(x[g][1]), "+v"(x[g][2]), "+v"(x[g][3]), "+v"(x[g][4]), "+v"(x[g][5]),
-                           "+v"(x[g][6]), "+v"(x[g][7]), "+v"(x[g][8]), "+v"(x[g][9]), "+v"(x[g][10]), "+v"(x[g][11]),
-                           "+v"(x[g][12]), "+v"(x[g][13]), "+v"(x[g][14]), "+v"(x[g][15])
-                         :
-                         : "memory");
-#endif
         float2 wv[16];
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             wv[2 * c] = make_float2(w4[c].x, w4[c].y);
             wv[2 * c + 1] = make_float2(w4[c].z, w4[c].w);
         }
-        EWK_TS(p1);
-        if (tim) EWK_TACC(8, p0, p1);
-#if EWK_PRIO
-        EWK_SETPRIO(EWK_PRIO == 1 ? 1 : 0);
-#endif
+        EWK_SETPRIO(0);
         // ---- DFT16 over n1 (window folded into its first stage), twiddle W256^(j*k1)
         // (one twiddle row serves every frame of the lane, requested before the DFT16s)
         EWK_LD128_8(t4, (uint32_t)(uintptr_t)(reinterpret_cast<const float4*>(smem + L_TW1) + j * (TP / 2)));
@@ -525,7 +465,6 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     // next pass's samples: issued before the mel stage (registers are free there),
     // stored to the staging area at the end of the pass
     float pf[kStageLoads];
-    EWK_TS(p2);
     {
         EWK_WAIT_8(t4);
 #pragma unroll
@@ -538,54 +477,17 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
             }
         }
     }
-#if EWK_PRIO
-    EWK_SETPRIO(EWK_PRIO == 1 ? 0 : 1);
-#endif
-    EWK_TS(p3);
-    if (tim) EWK_TACC(10, p2, p3);
+    EWK_SETPRIO(1);
     // ---- transpose through LDS (real, then imaginary half): lane k1 <- A_{n2}[k1].
     // Row r (16 floats) keeps column n in 4-float chunk (n>>2) ^ ((r>>2)&3): the
     // column writes (ds_write_b32, the frames of a 32-lane half 272 floats apart) and
     // the row reads (ds_read_b128) are both bank-conflict free.
-#if EWK_ABLATE & 64
-    {   // sensitivity probe: EWK_XLDS extra ds_read_b128 per pass (4 LDS cycles each)
-        floatx4 d;
-        const uint32_t da = (uint32_t)(uintptr_t)(smem + L_DCT) + 16 * j;
-#pragma unroll
-        for (int i = 0; i < EWK_XLDS; ++i) asm volatile("ds_read_b128 %0, %1" : "=v"(d) : "v"(da) : "memory");
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(d) : : "memory");
-        asm volatile("" : : "v"(d));
-    }
-#endif
-#if EWK_ABLATE & 128
-    {   // sensitivity probe: EWK_XVALU extra independent VALU ops per pass (4 chains)
-        float q0 = a[0][1].x, q1 = a[0][2].x, q2 = a[1][1].x, q3 = a[1][2].x;
-#pragma unroll
-        for (int i = 0; i < EWK_XVALU / 4; ++i) {
-            asm volatile("v_add_f32 %0, %0, %0" : "+v"(q0)); asm volatile("v_add_f32 %0, %0, %0" : "+v"(q1));
-            asm volatile("v_add_f32 %0, %0, %0" : "+v"(q2)); asm volatile("v_add_f32 %0, %0, %0" : "+v"(q3));
-        }
-        asm volatile("" : : "v"(q0), "v"(q1), "v"(q2), "v"(q3));
-    }
-#endif
     float2 b[kNF][16];
-#if EWK_ABLATE & 2
-#pragma unroll
-    for (int g = 0; g < kNF; ++g)
-#pragma unroll
-        for (int k1 = 0; k1 < 16; ++k1) b[g][k1] = a[g][dperm(k1)];
-#else
     {
-#if EWK_PAIR
         const uint32_t m0base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)scr);
         const int offA = tr_off(rowA, j >> 3) + 16 * f, offB = tr_off(rowB, j >> 3) + 16 * f;
-#else
-        const int jc = 4 * (j >> 2), jl = j & 3;
-        const int rsw = (j >> 2) & 3;
-#endif
 #pragma unroll
         for (int half = 0; half < 2; ++half) {
-#if EWK_PAIR
 #pragma unroll
             for (int g = 0; g < kNF; ++g) {
                 float w[16];
@@ -617,17 +519,7 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
                                [o15] "i"(4 * tr_off(15, g))
                              : "memory");
             }
-#else
-#pragma unroll
-            for (int g = 0; g < kNF; ++g)
-#pragma unroll
-                for (int k1 = 0; k1 < 16; ++k1) {
-                    const float2 vv = a[g][dperm(k1)];
-                    sc[g][16 * k1 + (jc ^ (4 * ((k1 >> 2) & 3))) + jl] = half ? vv.y : vv.x;
-                }
-#endif
             lds_order();
-#if EWK_PAIR
             // lane (h, j') = (j >> 3, j & 7) reads two columns of frame 4h + f: c0 = j' and its
             // conjugate partner 16 - j' (column 8 beside column 0 for j' = 0)
 #pragma unroll
@@ -643,36 +535,13 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
                     }
                 }
             }
-#else
-#pragma unroll
-            for (int g = 0; g < kNF; ++g) {
-                const float4* rd = reinterpret_cast<const float4*>(sc[g] + 16 * j);
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const float4 r = rd[c ^ rsw];
-                    if (half) {
-                        b[g][4 * c].y = r.x; b[g][4 * c + 1].y = r.y; b[g][4 * c + 2].y = r.z; b[g][4 * c + 3].y = r.w;
-                    } else {
-                        b[g][4 * c].x = r.x; b[g][4 * c + 1].x = r.y; b[g][4 * c + 2].x = r.z; b[g][4 * c + 3].x = r.w;
-                    }
-                }
-            }
-#endif
             lds_order();
         }
     }
-#endif
-#if EWK_PRIO
-    EWK_SETPRIO(EWK_PRIO == 1 ? 1 : 0);
-#endif
-    EWK_TS(p4);
-    if (tim) EWK_TACC(11, p3, p4);
+    EWK_SETPRIO(0);
     // ---- DFT16 over n2: Z[j + 16*k2] = b[dperm(k2)]
 #pragma unroll
     for (int g = 0; g < kNF; ++g) dft16_perm(b[g]);
-    EWK_TS(p5);
-    if (tim) EWK_TACC(12, p4, p5);
-#if EWK_PAIR
     // ---- untangle + power, two conjugate bins per step, no cross-lane traffic.  For
     // k = c0 + 16 it the partner Zp = Z[256 - k] sits in this lane's other column; with
     // A = Z[k] + conj(Zp), B = Z[k] - conj(Zp), C = i W512^k B:
@@ -750,51 +619,8 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
         scf[257 + jp] = 0.0f;
         if (jp < 7) scf[265 + jp] = 0.0f;
     }
-#else
-    // ---- untangle + power, one bin column at a time.  Partner Z[(256-k) & 255] of
-    // k = j + 16*k2 comes straight from the partner lane's registers: for j >= 1 it is
-    // lane 16-j's slot 15-k2 (DPP row_mirror then row_shr:1); lane 0 keeps its own
-    // slot (16-k2)&15.  P'[k] = |2 X[k]|^2 = |A - i W512^k B|^2 with
-    // A = Z[k] + conj(Zp), B = Z[k] - conj(Zp).
-    {
-        const float4* c4 = reinterpret_cast<const float4*>(smem + L_TW2) + j * (TP / 2);
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const float4 w = c4[c];
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {
-                const int k2 = 2 * c + u;
-                const float2 cs = u ? make_float2(w.z, w.w) : make_float2(w.x, w.y);
-#pragma unroll
-                for (int g = 0; g < kNF; ++g) {
-                    const float2 src = b[g][dperm(15 - k2)], own = b[g][dperm((16 - k2) & 15)];
-                    const int mx = __builtin_amdgcn_mov_dpp(__float_as_int(src.x), 0x140, 0xf, 0xf, false);   // row_mirror
-                    const int my = __builtin_amdgcn_mov_dpp(__float_as_int(src.y), 0x140, 0xf, 0xf, false);
-                    const float px = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.x), mx, 0x111, 0xf, 0xf, false));
-                    const float py = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(own.y), my, 0x111, 0xf, 0xf, false));
-                    const float2 z = b[g][dperm(k2)];
-                    const float ar = z.x + px, ai = z.y - py;
-                    const float br = z.x - px, bi = z.y + py;
-                    const float yr = ar - cs.y * br + cs.x * bi;
-                    const float yi = ai - cs.y * bi - cs.x * br;
-                    sc[g][j + 16 * k2] = yr * yr + yi * yi;
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int g = 0; g < kNF; ++g) {   // bin 256 (X[256] = Re Z[0] - Im Z[0]) and the zero pad the band loops read past it
-        const float2 z0 = b[g][dperm(0)];
-        const float y = 2.0f * (z0.x - z0.y);
-        sc[g][256 + j] = (j == 0) ? y * y : 0.0f;
-    }
-#endif
     lds_order();
-#if EWK_PRIO
-    EWK_SETPRIO(EWK_PRIO == 1 ? 0 : 1);
-#endif
-    EWK_TS(p6);
-    if (tim) EWK_TACC(13, p5, p6);
+    EWK_SETPRIO(1);
     if (next) stage_load(v, (t0 + kFPP) * HOP - NFFT / 2, lane, pf);
     // ---- mel + log: lane j computes bands m = j + 16*i of its frames (weights shared).
     // The stage's LDS reads go in two batches (band groups 0-5, then 6-7: 19 and 21
@@ -840,11 +666,7 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
                 }
         }
     }
-#if EWK_PRIO == 2
     EWK_SETPRIO(0);
-#endif
-    EWK_TS(p7);
-    if (tim) EWK_TACC(14, p6, p7);
     lds_order();
     // Rows of frames past T keep their (finite: silence gives -100 dB) values: the DCT
     // columns are independent and the statistics skip those frames, so only the frame's
@@ -852,7 +674,7 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     // k-chunk j of its frame row (hi and lo halves, one ds_write_b128 each).
 #pragma unroll
     for (int g = 0; g < kNF; ++g) {
-        const int r = row0 + (EWK_FPAIR ? 2 * f + g : 4 * g + f);
+        const int r = row0 + 2 * f + g;
         float fmx = db[g][0], fmn = db[g][0], x[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
@@ -869,12 +691,8 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
         *reinterpret_cast<uint4*>(tb + 256) = lo;
     }
     lds_order();
-    EWK_TS(p8);
-    if (tim) EWK_TACC(15, p7, p8);
     if (next) stage_store(scr, lane, pf);
     lds_order();
-    EWK_TS(p9);
-    if (tim) EWK_TACC(16, p8, p9);
 }
 
 // DCT of one 16-frame log-mel tile on the matrix cores: C[32 x 16] = D[32 x 128] X[128 x 16]
@@ -900,16 +718,12 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
                  : "memory")
 #define EWK_MF(a, b, acc) \
     acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8, a), __builtin_bit_cast(halfx8, b), acc, 0, 0, 0)
-#if EWK_ABLATE & 256   // timing probe: the DCT operands are read but only one MFMA per k-step runs
-#define EWK_DCT_MFMA(p) EWK_MF(A0h[p] + A1l[p], Bh[p] + Bl[p], acc0);
-#else
 #define EWK_DCT_MFMA(p)                                                                        \
     do {                                                                                       \
         EWK_MF(A0h[p], Bh[p], acc0); EWK_MF(A1h[p], Bh[p], acc1);                              \
         EWK_MF(A0h[p], Bl[p], acc0); EWK_MF(A1h[p], Bl[p], acc1);                              \
         EWK_MF(A0l[p], Bh[p], acc0); EWK_MF(A1l[p], Bh[p], acc1);                              \
     } while (0)
-#endif
 __device__ __forceinline__ void tile_dct(const float* tile, const float* s_dct, int lane, float (&c)[8]) {
     const int col = lane & 15, g4 = lane >> 4;
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -1061,7 +875,7 @@ __device__ __forceinline__ void zero_rows(float* tile, int row0, int lane) {
 template <int RING>
 __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, float* scr, float* tile,
                               float* tmins, float4* gscr, int scr_tiles, int lane, const int (&lo)[8],
-                              double (&s1)[8], double (&s2)[8], uint64_t* tim) {
+                              double (&s1)[8], double (&s2)[8]) {
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     const int T = 1 + v.len / HOP;
     const int ntile = (T + 15) >> 4;
@@ -1087,19 +901,16 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         // `run` is exact when the segment max is already known and is fixed up from its
         // parked (partly clamped) copy otherwise
         const float run = park ? wave_max(vmax) - 80.0f : -INFINITY;
-        EWK_TS(t0);
 #pragma unroll 1
         for (int p = 0; p < 16 / kFPP; ++p) {
             const int pass = tile_i * (16 / kFPP) + p;
             if (pass < npass)
                 frame_pass(v, pass * kFPP, T, p * kFPP, pass + 1 < npass, smem, scr, tile, lane, lo, vmax, tmin,
-                           run, tim);
+                           run);
             else   // rows of frames past T: zero (ignored by the statistics)
                 zero_rows(tile, p * kFPP, lane);
         }
         lds_order();
-        EWK_TS(t1);
-        EWK_TACC(0, t0, t1);
         if (park) {   // all 8 reads in flight, then the stores
             float4* dst = gscr + (int64_t)tile_i * 8 * 64 + lane;
             floatx4 t[8];
@@ -1123,15 +934,11 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         vmin = fminf(vmin, tmin);
         tmin = fmaxf(wave_min(tmin), run);   // the stored tile's minimum
         if (lane == 0) tmins[min(tile_i, kLmTiles - 1)] = tmin;   // kLmTiles slots: only the parked path reads them
-        EWK_TS(t2);
-        EWK_TACC(1, t1, t2);
     }
-    EWK_TS(t3);
     // wave-wide log-mel max/min
     vmax = wave_max(vmax);
     vmin = wave_min(vmin);
     const float theta = vmax - 80.0f;
-#if !(EWK_ABLATE & 32)
     if (vmin < theta) {
         lds_order();
         if (park) {
@@ -1190,12 +997,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
             }
         }
     }
-#endif
-    EWK_TS(t4);
-    EWK_TACC(2, t3, t4);
     finish_stats(T, cref, s1, s2, lane, reinterpret_cast<double*>(scr));
-    EWK_TS(t5);
-    EWK_TACC(3, t4, t5);
 }
 
 
@@ -1483,8 +1285,11 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, fl
     }
 }
 
-template <int RING>
-__global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const Tables* __restrict__ tab, ScoreArgs a) {
+// MODE 0: linear batch; 1: ring events, one segment per workgroup (cooperative); 2: ring
+// events, one segment per wave from the work counter.
+template <int MODE>
+__global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __restrict__ tab, ScoreArgs a) {
+    constexpr int RING = MODE != 0;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // ring mode: the event window and this workgroup's first event, requested before the
     // table fill so their latency overlaps it
@@ -1504,18 +1309,13 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
             const int j = i & 15, n = i >> 4;   // win2[16n + j], tw1[16n + j], tw2[j + 16n]
             sw2[j * TP + n] = tab->win2[i];
             if (n > 0) st1[j * TP + n - 1] = tab->tw1[i];
-#if !EWK_PAIR
-            st2[j * TP + n] = tab->tw2[i];
-#endif
         }
-#if EWK_PAIR
         // [j'][it] = tw2[k] for the bin k that lane class j' untangles at step it
         for (int i = threadIdx.x; i < 8 * 17; i += blockDim.x) {
             const int jp = i / 17, it = i % 17;
             const int k = jp ? jp + 16 * (it < 16 ? it : 15) : (it <= 8 ? 16 * it : 8 + 16 * (it - 9));
             st2[jp * TP + it] = tab->tw2[k];
         }
-#endif
         int* sb = reinterpret_cast<int*>(smem + L_BLO);
         for (int i = threadIdx.x; i < NMEL; i += blockDim.x) sb[i] = tab->band_lo[i];
         float* sw = reinterpret_cast<float*>(smem + L_WPAD);
@@ -1573,18 +1373,16 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
         for (int i = 0; i < 8; ++i) lo[i] = sb[(lane & 15) + 16 * i];
     }
     // persistent waves pull segments from a work counter (ragged lengths balance)
-#if EWK_TIMING
-    uint64_t tim[17] = {};
-    EWK_TS(t_begin);
-#else
-    uint64_t* tim = nullptr;
-#endif
     // the template is loop-invariant: fetched once, off every segment's critical path.
     // (Reserving the next work item ahead was tried: the tail imbalance costs more.)
     const bool act = lane < NMFCC;
     const float tmf = (a.has_template && act) ? a.tmpl[lane] : 0.0f;
     const float tsf = (a.has_template && act) ? a.tmpl[NMFCC + lane] : 0.0f;
-    if (RING) {   // one segment per workgroup at a time, its tiles spread over the waves
+    // Ring mode, MODE 1 (a tick of ~10^3-10^4 streams: a few hundred segments, latency
+    // bound): one segment per workgroup at a time, its tiles spread over the waves.  MODE 2
+    // (10^5-10^6 streams: enough events to keep every wave busy) falls through: the waves
+    // take whole segments from the work counter, like a linear batch.
+    if (MODE == 1) {
         int* wg_idx = reinterpret_cast<int*>(smem + L_WG);
         float* misc0 = reinterpret_cast<float*>(smem + L_SCR);   // wave 0's FFT scratch (epilogue only)
         (void)wg_idx;
@@ -1605,7 +1403,6 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
         return;
     }
     for (;;) {
-        EWK_TS(ta);
         int idx = 0;
         if (lane == 0) idx = atomicAdd(a.work, 1);
         idx = __shfl(idx, 0, 64);
@@ -1630,10 +1427,7 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
         const SegSrc<RING> v = make_src<RING>(p, start, ring, len);
 
         double st1[8], st2[8];
-        EWK_TS(tb);
-        EWK_TACC(4, ta, tb);
-        segment_stats(v, smem, scr, tile, tmins, gscr, a.lm_tiles, lane, lo, st1, st2, tim);
-        EWK_TS(tc);
+        segment_stats(v, smem, scr, tile, tmins, gscr, a.lm_tiles, lane, lo, st1, st2);
 
         // ---- lane k < 20 holds coefficient k's mean / std (fp32-rounded like the reference's)
         const float cmf = act ? (float)st1[0] : 0.0f, csf = act ? (float)st2[0] : 0.0f;
@@ -1643,17 +1437,7 @@ __global__ __launch_bounds__(64 * WAVES, kScoreWGsPerCU) void k_score_f32(const 
         }
         if (a.has_template) score_epilogue<RING>(a, cmf, csf, tmf, tsf, lane, seg, v.len);
         lds_order();
-        EWK_TS(td);
-        EWK_TACC(5, tc, td);
     }   // work loop
-#if EWK_TIMING
-    EWK_TS(t_end);
-    EWK_TACC(6, t_begin, t_end);
-    if (lane == 0) {
-        for (int i = 0; i < 17; ++i) if (i != 7) atomicAdd(&g_tim[i], (unsigned long long)tim[i]);
-        atomicAdd(&g_tim[7], 1ull);
-    }
-#endif
 }
 
 // Ring-mode epilogue: advance the scored-event watermark and re-arm the ring-mode
@@ -1683,9 +1467,6 @@ hipError_t launch_snapshot(const int32_t* src, int32_t* dst, hipStream_t s) {
 // segments are the shortest, so the grid drains evenly): 64 buckets of the segment's pass
 // count, longest first; the order within a bucket is arbitrary (each segment's result
 // does not depend on it).
-#ifndef EWK_LPT
-#define EWK_LPT 1   // longest-first order for large linear batches (0: index order)
-#endif
 constexpr int kLptBuckets = 64;
 __device__ __forceinline__ int lpt_bucket(int32_t len) {   // longest first: bucket 0 = most passes
     const int np = (1 + max(len, 0) / HOP + kFPP - 1) / kFPP;
@@ -1745,12 +1526,14 @@ int score_grid(int n_seg, int ring_mode) {
 hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mode, hipStream_t s) {
     if (a.n_seg <= 0) return hipSuccess;
     const int grid = score_grid(a.n_seg, ring_mode);
-    if (ring_mode) {   // ring mode: the re-score launch re-arms the counter after each tick
+    if (ring_mode == 2) {   // ring mode: the re-score launch re-arms the counter after each tick
+        hipLaunchKernelGGL(k_score_f32<2>, dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
+    } else if (ring_mode) {
         hipLaunchKernelGGL(k_score_f32<1>, dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
     } else {
         ScoreArgs b = a;
         // the order only matters once the waves queue several segments each
-        if (EWK_LPT && a.order && a.n_seg > 2 * grid * WAVES) {
+        if (a.order && a.n_seg > 2 * grid * WAVES) {
             int32_t* cnt = a.order + a.n_seg;
             hipError_t e = hipMemsetAsync(cnt, 0, 2 * kLptBuckets * sizeof(int32_t), s);
             if (e != hipSuccess) return e;
@@ -2019,11 +1802,3 @@ hipError_t launch_score_f64(const Tables64* d_tab64, const ScoreArgs& a, int rin
 
 }  // namespace ewk
 
-#if EWK_TIMING
-// per-phase cycle totals of k_score_f32 since the last call (timing builds only)
-extern "C" int ewk_debug_timing(unsigned long long* out) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ewk::g_tim), 24 * sizeof(unsigned long long)) != hipSuccess) return -3;
-    unsigned long long z[24] = {};
-    return hipMemcpyToSymbol(HIP_SYMBOL(ewk::g_tim), z, sizeof(z)) == hipSuccess ? 0 : -3;
-}
-#endif

@@ -1,7 +1,7 @@
 """Gate microbenchmark: k_gate_ticks alone on the streaming recipe (one tick per launch).
-Usage: python scripts/mb_gate.py [streams] [ticks]   (EWK_LIB selects the .so variant; a
-timing build -DEWK_GATE_TIMING=1 also prints per-phase cycles per wave)."""
-import ctypes, os, sys
+Usage: python scripts/mb_gate.py [streams] [ticks]   (EWK_LIB selects the .so variant, e.g. one
+built by scripts/build_variant.sh from another revision)."""
+import os, sys
 import numpy as np
 ROOT = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
@@ -25,11 +25,6 @@ for t in range(120):                       # prefill + detection start
     se.poll()
 se.sync()
 libname = os.environ.get("EWK_LIB") or os.path.join(ROOT, "easywakeword_amd", "libewk.so")
-lib = ctypes.CDLL(libname)
-timing = hasattr(lib, "ewk_debug_gate_timing")
-buf = (ctypes.c_ulonglong * 16)()
-if timing:
-    lib.ewk_debug_gate_timing(buf)
 se.profile(True)
 for t in range(120, 120 + ticks):
     se.push_device(base + (t % 160) * 1600 * 4, P + pad, 1600, 1)
@@ -38,8 +33,3 @@ se.poll()
 se.sync()
 ms, k = se.profile_read(2)
 print(f"{os.path.basename(libname):24s} pad {pad:4d} gate {ms / max(1, k) * 1e3:7.1f} us/tick over {k} ticks, {n} streams")
-if timing:
-    lib.ewk_debug_gate_timing(buf)
-    w = max(1, buf[7])
-    names = ["load state+regs", "ingest", "threshold (a2)", "is_silent (a3)", "tick loop", "store", "wave life"]
-    print("  per-wave cycles: " + ", ".join(f"{nm}={buf[i] / w:,.0f}" for i, nm in enumerate(names)))
