@@ -1,10 +1,13 @@
 """Audio I/O for the drop-in facade: WAV decode and block sources.
 
-``load_wav`` replaces ``librosa.load(path, sr=16000)`` for 16 kHz files
-(reference wakeword.py:588): PCM16 -> float32 int16/32768 (libsndfile
-scaling), PCM32 -> /2**31, IEEE float32 as is, channel mean for
-multi-channel files (librosa.to_mono).  Other sample rates need librosa's soxr
-resampler, which is out of scope: they raise ValueError.
+``load_wav`` replaces ``librosa.load(path, sr=16000)`` (reference wakeword.py:588,
+866-870): PCM16 -> float32 int16/32768 (libsndfile scaling), PCM32 -> /2**31,
+8-bit unsigned -> (x-128)/128, channel mean for multi-channel files
+(librosa.to_mono).  16 kHz files are bit-exact with librosa.  Other rates are
+resampled to 16 kHz on the host with a polyphase Kaiser FIR
+(scipy.signal.resample_poly); librosa's default there is soxr 'HQ' (soxr is absent
+from this image), so resampled audio is close to, not bit-identical with, the
+reference's -- parity unpinned for non-16 kHz files.
 
 Sources replace the PortAudio input stream of SoundBuffer (wakeword.py:438-444):
 each yields float32 blocks of ``block`` samples, one per 0.1 s tick.
@@ -23,9 +26,6 @@ def load_wav(path: str, sr: int = FREQUENCY) -> np.ndarray:
     with wave.open(str(path), "rb") as w:
         nch, sw, rate, n = w.getnchannels(), w.getsampwidth(), w.getframerate(), w.getnframes()
         raw = w.readframes(n)
-    if rate != sr:
-        raise ValueError(f"{path}: sample rate {rate} Hz; only {sr} Hz files are supported "
-                         "(resampling is out of scope)")
     if sw == 2:
         x = np.frombuffer(raw, dtype="<i2").astype(np.float32) / np.float32(32768.0)
     elif sw == 4:
@@ -36,7 +36,23 @@ def load_wav(path: str, sr: int = FREQUENCY) -> np.ndarray:
         raise ValueError(f"{path}: unsupported sample width {sw}")
     if nch > 1:
         x = np.mean(x.reshape(-1, nch).T, axis=0).astype(np.float32)
+    if rate != sr:
+        x = resample(x, rate, sr)
     return np.ascontiguousarray(x, dtype=np.float32)
+
+
+def resample(x: np.ndarray, orig_sr: int, target_sr: int) -> np.ndarray:
+    """Band-limited resampling orig_sr -> target_sr (polyphase FIR, Kaiser beta 5.0),
+    float64 internally, float32 out, length ceil(n * target / orig) like librosa."""
+    from math import gcd
+    from scipy.signal import resample_poly
+    if orig_sr <= 0 or target_sr <= 0:
+        raise ValueError("sample rates must be positive")
+    g = gcd(int(orig_sr), int(target_sr))
+    up, down = int(target_sr) // g, int(orig_sr) // g
+    y = resample_poly(np.asarray(x, np.float64), up, down, window=("kaiser", 5.0))
+    n = int(np.ceil(len(x) * target_sr / orig_sr))
+    return y[:n].astype(np.float32)
 
 
 def write_wav(path: str, audio, sr: int = FREQUENCY) -> None:

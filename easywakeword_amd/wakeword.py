@@ -51,11 +51,16 @@ BLOCK = 1600
 class WordMatcher:
     """MFCC + cosine matcher (reference wakeword.py:520-639) on the GPU scorer.
 
-    ``extract_mfcc`` returns float32 mean/std of librosa-equivalent MFCCs
-    (n_mfcc=20, n_fft=512, hop=160).  Float64 input is computed at float32
-    precision (scores agree with the reference's float64 path within 1e-4; a
-    decision within ``rescore_margin`` of the threshold is re-scored in float64
-    on the device)."""
+    ``extract_mfcc`` returns the mean/std of librosa-equivalent MFCCs (n_mfcc=20,
+    n_fft=512, hop=160) in the input's dtype like the reference: float32 input on the
+    fp32 scorer, float64 input on the device's fp64 path (k_score_f64, within 1e-9 of
+    the float64 reference).  ``calculate_similarity`` / ``matches`` score on the fp32
+    scorer (within 1e-4 of the reference; a score within ``rescore_margin`` of the
+    threshold is re-scored in float64 on the device, so decisions are exact).
+
+    A matcher built with ``engine=`` shares that engine's threshold: ``matches(audio,
+    threshold)`` with another threshold changes it (WakeWord gives its matcher an
+    engine of its own)."""
 
     def __init__(self, sample_rate: int = FREQUENCY, gpu: int = 0, engine: Optional[Engine] = None) -> None:
         if sample_rate != FREQUENCY:
@@ -71,6 +76,10 @@ class WordMatcher:
         return self._engine
 
     def extract_mfcc(self, audio: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        a = np.asarray(audio)
+        if a.dtype == np.float64:   # the reference's float64 candidate path (wakeword.py:544-567)
+            m, s, _ = self._engine.score_f64([a])
+            return m[0], s[0]
         m, s, _, _ = self._engine.score([audio], require_template=False)
         return m[0], s[0]
 

@@ -201,3 +201,18 @@ def test_speculative_top_db_clamp(engine):
         ref = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
         assert score_close(score[i], ref, SCORE_TOL), (i, len(x), score[i], ref)
         assert bool(match[i]) == (ref >= 75.0)
+
+
+def test_extract_mfcc_keeps_the_input_dtype():
+    """float64 input returns float64 stats like the reference (the device's
+    fp64 path, within 1e-9 of the float64 oracle); float32 input returns float32."""
+    from easywakeword_amd import WordMatcher
+    m = WordMatcher()
+    for x in (synth.load_word(), synth.speech_like(), synth.ragged_segments(77, 1, 20000, 20000)[0]):
+        m64, s64 = m.extract_mfcc(x.astype(np.float64))
+        assert m64.dtype == np.float64 and s64.dtype == np.float64
+        rm, rs = mfcc_ref.extract_mfcc(x.astype(np.float64))
+        np.testing.assert_allclose(m64, rm, rtol=0, atol=1e-9 * max(1.0, float(np.abs(rm).max())))
+        np.testing.assert_allclose(s64, rs, rtol=0, atol=1e-9 * max(1.0, float(np.abs(rs).max())))
+        m32, s32 = m.extract_mfcc(x.astype(np.float32))
+        assert m32.dtype == np.float32 and s32.dtype == np.float32
