@@ -25,8 +25,9 @@ per MFCC frame, HIP-event timed), ``cpu_baseline`` (oracle/mfcc_ref.py, the
 librosa-0.11 restatement, on rank 0 at N=1 only, time-bounded sample),
 ``streaming`` (configs[2]: 8192 streams through the full level-1 + level-2
 engine, one tick per push), ``streaming_100k`` (131,072 resident streams with the
-reference's 10 s rings) and ``streaming_max`` (as many resident streams as HBM holds
-with compact 3 s sample rings, default 1,048,576): measured ms per tick, never
+reference's 10 s rings) and ``streaming_max`` (as many resident streams as HBM holds,
+default up to 2,097,152, with compact 3 s int16 rings fed int16 PCM -- what a PCM16
+microphone delivers, stored exactly): measured ms per tick, never
 extrapolated -- ``streams_realtime`` is the resident count when every tick of every
 stream finished inside the 100 ms tick budget.
 """
@@ -68,9 +69,11 @@ def parse():
     ap.add_argument("--stream-ticks", type=int, default=600, help="ticks after the 10 s prefill")
     ap.add_argument("--big-streams", type=int, default=131072,
                     help="north-star run: streams resident with the reference's full 10 s rings (0 = skip)")
-    ap.add_argument("--max-streams", type=int, default=1048576,
-                    help="streams resident with compact sample rings, capped by free HBM (0 = skip)")
+    ap.add_argument("--max-streams", type=int, default=2097152,
+                    help="streams resident with compact int16 sample rings, capped by free HBM (0 = skip)")
     ap.add_argument("--max-ring", type=int, default=48000, help="compact ring samples per stream (3 s)")
+    ap.add_argument("--max-float32", action="store_true",
+                    help="streaming_max with float32 input and rings instead of int16 PCM")
     ap.add_argument("--big-ticks", type=int, default=300, help="ticks after the prefill for the big runs")
     ap.add_argument("--fixed-len", type=int, default=16000,
                     help="also time the scorer on segments of this one length (0 = skip)")
@@ -338,7 +341,7 @@ def make_streams(torch, dev, n_streams, seed, word):
     return period_ticks, pcm
 
 
-def make_shifted_signal(torch, dev, n_streams, n_ticks, seed, word):
+def make_shifted_signal(torch, dev, n_streams, n_ticks, seed, word, pcm16=False):
     """Input for very many streams in bounded memory: one long synthetic signal of
     n_streams + n_ticks ticks (N(0, sigma) noise, sigma redrawn every 16 s, an event every
     U(2.4, 4.0) s: half words, half distractors, gain U(0.3, 2)); stream s hears it from
@@ -368,37 +371,49 @@ def make_shifted_signal(torch, dev, n_streams, n_ticks, seed, word):
         c1 = min(len(pos), c0 + 4096)
         idx = torch.from_numpy(pos[c0:c1]).to(dev)[:, None] + ar[None, :]
         sig.index_put_((idx.reshape(-1),), (table[kind[c0:c1]] * gain[c0:c1, None]).reshape(-1), accumulate=True)
+    if pcm16:   # what a PCM16 microphone delivers: round(x * 32768), saturated (the float copy is freed)
+        q = torch.empty(sig.numel(), device=dev, dtype=torch.int16)
+        for i0 in range(0, sig.numel(), 1 << 28):
+            i1 = min(sig.numel(), i0 + (1 << 28))
+            q[i0:i1] = torch.round(sig[i0:i1] * 32768.0).clamp_(-32768, 32767).to(torch.int16)
+        del sig
+        torch.cuda.empty_cache()
+        sig = q
     torch.cuda.synchronize()
     return sig
 
 
-def fit_streams(torch, dev, ring_samples, signal_ticks, reserve=8 << 30):
+def fit_streams(torch, dev, ring_samples, signal_ticks, reserve=8 << 30, sample_bytes=4):
     """Largest multiple of 65,536 streams whose engine + shared input signal fit in the
-    free HBM (ring, block-RMS arrays, state, two event banks, 6.4 KB of signal each)."""
+    free HBM (ring, block-RMS arrays, state, two event banks, one tick of signal each;
+    an int16 signal's float32 staging is freed before the engine is built)."""
     free, _ = torch.cuda.mem_get_info(dev)
-    per = ring_samples * 4 + 3 * (10 * SR // 1600) * 8 + 96 + 2 * 4 * 48 + 1600 * 4
-    n = int((free - reserve - signal_ticks * 1600 * 4) // per)
+    per = ring_samples * sample_bytes + 3 * (10 * SR // 1600) * 8 + 96 + 2 * 4 * 48 + 1600 * sample_bytes
+    n = int((free - reserve - signal_ticks * 1600 * sample_bytes) // per)
     return max(65536, n // 65536 * 65536)
 
 
 def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1, first_stream=0, cdev=None,
-                    confirm_batch=0, ring_samples=0, shifted=False, prof_ticks=200):
+                    confirm_batch=0, ring_samples=0, shifted=False, prof_ticks=200, pcm16=False):
     """Full level-1 + level-2 engine on `n_streams` RESIDENT synthetic streams: 10 s
     prefill, then `n_ticks` ticks launched one at a time (the real-time cadence).
     shifted=False: a private 16 s loop per stream (make_streams); True: the shared
     long signal of make_shifted_signal (for 10^5-10^6 streams).  ring_samples > 0:
-    compact sample rings (ewk_config.ring_samples; same events and scores).
+    compact sample rings (ewk_config.ring_samples; same events and scores).  pcm16: int16
+    PCM input (shifted signal only) into int16 rings (EWK_RING_I16, exact; half the bytes).
     With world > 1 every tick also gathers the ranks' positive detections
     {stream, tick, length, score} to rank 0 over RCCL (easywakeword_amd.shard.gather_positives)."""
     prof_ticks = min(prof_ticks, n_ticks)
     if shifted:
-        pcm = make_shifted_signal(torch, dev, n_streams, 100 + n_ticks + prof_ticks, seed, word)
+        pcm = make_shifted_signal(torch, dev, n_streams, 100 + n_ticks + prof_ticks, seed, word, pcm16=pcm16)
         period_ticks, stride = None, 1600
     else:
         period_ticks, pcm = make_streams(torch, dev, n_streams, seed, word)
         stride = period_ticks * 1600
     se = eng_mod.StreamEngine(n_streams, gpu=dev.index if dev.index is not None else 0,
-                              ring_samples=int(ring_samples))
+                              ring_samples=int(ring_samples), ring_format=1 if pcm16 else 0)
+    push = se.push_device_pcm16 if pcm16 else se.push_device
+    es = 2 if pcm16 else 4
     se.template_from_pcm(word)
     base = pcm.data_ptr()
 
@@ -418,7 +433,7 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
             else:
                 k = t % period_ticks
                 n = min(per_call, nt - (t - t0), period_ticks - k)
-            se.push_device(base + k * 1600 * 4, stride, 1600, n)
+            push(base + k * 1600 * es, stride, 1600, n)
             # the host consumes detections every call; lagged: tick t-1's events while the GPU runs tick t
             ev = se.poll(lagged=lagged)
             events.append(ev)
@@ -454,9 +469,10 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
     gate_ms_tick = gate_ms / max(1, gate_n)
     ring = int(ring_samples) if ring_samples else 10 * SR
     out = {"streams": n_streams, "resident": True, "ticks": n_ticks, "audio_seconds_per_stream": n_ticks * 0.1,
-           "input": "shared long signal, stream s from tick s (make_shifted_signal)" if shifted
-                    else "private 16 s loop per stream (make_streams)",
-           "ring_samples_per_stream": ring, "ring_bytes_total": ring * 4 * n_streams,
+           "input": ("shared long signal, stream s from tick s (make_shifted_signal)" if shifted
+                     else "private 16 s loop per stream (make_streams)") + (", int16 PCM" if pcm16 else ", float32"),
+           "ring_samples_per_stream": ring, "ring_format": "int16" if pcm16 else "float32",
+           "ring_bytes_total": ring * es * n_streams,
            "wall_s": wall, "ms_per_tick": per_tick * 1e3,
            "realtime": per_tick <= 0.1,
            "realtime_headroom": 0.1 / per_tick,
@@ -649,14 +665,16 @@ def main():
                              confirm_batch=args.confirm_batch if rank == 0 else 0)
         out["streaming"] = st
         best = st["streams_realtime"]
-        for key, n_req, ring in (("streaming_100k", args.big_streams, 0),
-                                 ("streaming_max", args.max_streams, args.max_ring)):
+        for key, n_req, ring, p16 in (("streaming_100k", args.big_streams, 0, False),
+                                      ("streaming_max", args.max_streams, args.max_ring, not args.max_float32)):
             if n_req <= 0:
                 continue
             torch.cuda.empty_cache()
-            n = min(n_req, fit_streams(torch, dev, ring or 10 * SR, 100 + 2 * args.big_ticks))
+            n = min(n_req, fit_streams(torch, dev, ring or 10 * SR, 100 + 2 * args.big_ticks,
+                                       sample_bytes=2 if p16 else 4))
             r = streaming_bench(torch, dev, ewa, n, args.big_ticks, args.seed + 31 * rank, word, world=world,
-                                first_stream=rank * n, cdev=cdev, ring_samples=ring, shifted=True, prof_ticks=50)
+                                first_stream=rank * n, cdev=cdev, ring_samples=ring, shifted=True, prof_ticks=50,
+                                pcm16=p16)
             r["requested_streams"] = n_req
             out[key] = r
             best = max(best, r["streams_realtime"])

@@ -27,6 +27,8 @@ EWK_EV_RESCORED = 2
 EWK_PUSH_DEVICE = 1
 EWK_PCM_DEVICE = 1
 EWK_OUT_DEVICE = 4
+EWK_RING_F32 = 0
+EWK_RING_I16 = 1
 EWK_SCORE_REQUIRE_TEMPLATE = 1
 EWK_SCORE_F32_CANDIDATES = 2
 
@@ -52,6 +54,7 @@ class EwkConfig(C.Structure):
         ("post_speech_silence", C.c_double), ("padding", C.c_double), ("max_segment_seconds", C.c_double),
         ("similarity_threshold", C.c_double), ("reentry_timeout", C.c_double), ("min_threshold", C.c_double),
         ("initial_threshold", C.c_double), ("rescore_margin", C.c_double),
+        ("ring_format", C.c_int32), ("reserved1", C.c_int32),
     ]
 
 

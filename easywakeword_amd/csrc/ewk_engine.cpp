@@ -99,7 +99,10 @@ struct ewk_engine {
     DevBuf<double> mean64, std64;
 
     // streaming
-    float* d_ring = nullptr;
+    void* d_ring = nullptr;         // float32 or int16 samples (cfg.ring_format)
+    size_t ring_es = sizeof(float); // bytes per ring sample
+    float* ring_f32() const { return ring_es == sizeof(float) ? static_cast<float*>(d_ring) : nullptr; }
+    int16_t* ring_i16() const { return ring_es == sizeof(int16_t) ? static_cast<int16_t*>(d_ring) : nullptr; }
     double* d_brms = nullptr;
     double* d_sorted = nullptr;     // [streams][2][n_blocks] sorted block RMS (double-buffered)
     PwTree* d_trees = nullptr;      // numpy pairwise-sum trees for the block and the last 0.1 s
@@ -324,6 +327,8 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
         return fail(EWK_EINVAL, "speech_duration_min must be <= speech_duration_max");
     if (c.post_speech_silence <= 0) return fail(EWK_EINVAL, "post_speech_silence must be positive");
     if (n_streams < 0) return fail(EWK_EINVAL, "n_streams must be >= 0");
+    if (c.ring_format != EWK_RING_F32 && c.ring_format != EWK_RING_I16)
+        return fail(EWK_EINVAL, "ring_format must be EWK_RING_F32 or EWK_RING_I16");
     const int64_t ring_len = (int64_t)c.buffer_seconds * c.sample_rate;
     if (ring_len > INT32_MAX / 2) return fail(EWK_EINVAL, "buffer_seconds too large");
     // Longest segment request the cut can make (wakeword.py:1100-1111): nreq =
@@ -356,6 +361,7 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
     e->n_streams = n_streams;
     e->ring_len = ring_len;
     e->sring_len = c.ring_samples > 0 ? (int64_t)c.ring_samples : ring_len;
+    e->ring_es = c.ring_format == EWK_RING_I16 ? sizeof(int16_t) : sizeof(float);
     e->n_blocks = (int32_t)(e->ring_len / c.block);
     e->n_last = (int64_t)(0.1 * (double)c.sample_rate);   // int(0.1 * FREQUENCY)
     auto bail = [&](hipError_t err, const char* what) {
@@ -404,7 +410,7 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
         if ((err = e->f64_scratch.reserve((size_t)per * e->f64_grid)) != hipSuccess) return bail(err, "f64 scratch");
     }
     if (n_streams > 0) {
-        const size_t ring_bytes = (size_t)n_streams * e->sring_len * sizeof(float);
+        const size_t ring_bytes = (size_t)n_streams * e->sring_len * e->ring_es;
         if ((err = hipMalloc(&e->d_ring, ring_bytes)) != hipSuccess) return bail(err, "ring");
         if ((err = hipMalloc(&e->d_brms, (size_t)n_streams * std::max(1, e->n_blocks) * sizeof(double))) != hipSuccess)
             return bail(err, "block rms");
@@ -709,7 +715,7 @@ int ewk_reset_streams(ewk_engine* e) {
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = e->stream;
     HIP_TRY(join_scoring(e, s));
-    HIP_TRY(hipMemsetAsync(e->d_ring, 0, (size_t)e->n_streams * e->sring_len * sizeof(float), s));
+    HIP_TRY(hipMemsetAsync(e->d_ring, 0, (size_t)e->n_streams * e->sring_len * e->ring_es, s));
     HIP_TRY(hipMemsetAsync(e->d_brms, 0, (size_t)e->n_streams * std::max(1, e->n_blocks) * sizeof(double), s));
     std::vector<GateStream> st(e->n_streams);
     for (auto& x : st) {
@@ -731,7 +737,8 @@ int ewk_reset_streams(ewk_engine* e) {
 static int score_pending(ewk_engine* e, hipStream_t ss, const int32_t* n_events) {
     if (!e->has_tmpl) return EWK_OK;   // events keep NaN scores until a template exists
     ScoreArgs a = base_args(e);
-    a.pcm = e->d_ring;
+    a.pcm = e->ring_f32();
+    a.pcm16 = e->ring_i16();
     a.ring_len = e->sring_len;
     a.events = e->ev_bank(e->bank);
     a.n_events = n_events;
@@ -762,6 +769,8 @@ static int push_impl(ewk_engine* e, const void* pcm_any, int64_t stride, int64_t
     if (e->n_streams <= 0) return fail(EWK_EINVAL, "engine has no streams");
     if (!pcm_any) return fail(EWK_EINVAL, "pcm is NULL");
     if (n_ticks <= 0) return fail(EWK_EINVAL, "n_ticks must be positive");
+    if (!pcm16 && e->ring_es == sizeof(int16_t))
+        return fail(EWK_EINVAL, "an int16 ring (EWK_RING_I16) takes PCM16 pushes (ewk_push_pcm16)");
     const size_t es = pcm16 ? sizeof(int16_t) : sizeof(float);
     const unsigned char* pcm = static_cast<const unsigned char*>(pcm_any);
     if (stride < e->cfg.block && e->n_streams > 1) return fail(EWK_EINVAL, "stride must be >= block");
@@ -806,7 +815,8 @@ static int push_impl(ewk_engine* e, const void* pcm_any, int64_t stride, int64_t
         g.n_ticks = nt;
         g.n_streams = e->n_streams;
         g.tick0 = e->tick;
-        g.ring = e->d_ring;
+        g.ring = e->ring_f32();
+        g.ring16 = e->ring_i16();
         g.ring_len = e->ring_len;
         g.sring_len = e->sring_len;
         g.compact = e->sring_len < e->ring_len ? 1 : 0;
@@ -908,7 +918,8 @@ static int normalize_impl(ewk_engine* e, const float* d_pcm, const int64_t* offs
         HIP_TRY(d_ev.reserve(std::max<int32_t>(1, n)));
         HIP_TRY(hipMemcpyAsync(d_ev.p, events, n * sizeof(ewk_event), hipMemcpyHostToDevice, s));
         a.events = d_ev.p;
-        a.pcm = e->d_ring;
+        a.pcm = e->ring_f32();
+        a.pcm16 = e->ring_i16();
         a.ring_len = e->sring_len;
     } else {
         HIP_TRY(d_off.reserve(std::max<int32_t>(1, n)));
@@ -1148,12 +1159,19 @@ int ewk_read_segment(ewk_engine* e, int32_t stream, int64_t ring_start, int32_t 
     if (length < 0 || length > e->sring_len || ring_start < 0 || ring_start >= e->sring_len)
         return fail(EWK_EINVAL, "segment out of range");
     HIP_TRY(hipSetDevice(e->device));
-    const float* base = e->d_ring + (size_t)stream * e->sring_len;
+    const size_t es = e->ring_es;
+    const unsigned char* base = static_cast<const unsigned char*>(e->d_ring) + (size_t)stream * e->sring_len * es;
     const int64_t first = std::min<int64_t>(length, e->sring_len - ring_start);
-    HIP_TRY(hipMemcpyAsync(out, base + ring_start, first * sizeof(float), hipMemcpyDeviceToHost, e->stream));
+    // int16 rings are copied into the tail half of `out` and widened in place (x / 32768, exact)
+    unsigned char* dst = reinterpret_cast<unsigned char*>(out) + (es == sizeof(float) ? 0 : (size_t)length * 2);
+    HIP_TRY(hipMemcpyAsync(dst, base + ring_start * es, first * es, hipMemcpyDeviceToHost, e->stream));
     if (length > first)
-        HIP_TRY(hipMemcpyAsync(out + first, base, (length - first) * sizeof(float), hipMemcpyDeviceToHost, e->stream));
+        HIP_TRY(hipMemcpyAsync(dst + first * es, base, (length - first) * es, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
+    if (es == sizeof(int16_t)) {
+        const int16_t* q = reinterpret_cast<const int16_t*>(dst);
+        for (int32_t i = 0; i < length; ++i) out[i] = (float)q[i] * (1.0f / 32768.0f);
+    }
     return EWK_OK;
 }
 

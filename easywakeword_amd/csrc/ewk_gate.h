@@ -64,7 +64,8 @@ struct GateArgs {
     int32_t n_ticks;
     int32_t n_streams;
     int64_t tick0;           // ticks already delivered
-    float* ring;             // [n_streams][sring_len] sample rings
+    float* ring;             // [n_streams][sring_len] sample rings (float32) ...
+    int16_t* ring16;         // ... or int16 (EWK_RING_I16: PCM16 pushes stored as delivered)
     int64_t ring_len;        // the reference ring (buffer_seconds * sample_rate): blocks, pointer, fill
     int64_t sring_len;       // samples stored per stream (== ring_len, or a compact ring: see ewk_config.ring_samples)
     int32_t compact;         // sring_len < ring_len (block-aligned; block RMSs kept from the first write)

@@ -106,12 +106,13 @@ struct LdsSrc {
 
 struct RingSrc {
     const float* ring;
+    const int16_t* ring16;   // int16 ring (EWK_RING_I16) when set: value = x / 32768, exact
     int32_t first;   // physical index of element 0
     int32_t R;
     __device__ __forceinline__ float operator()(int i) const {
         int k = first + i;
         if (k >= R) k -= R;
-        return ring[k];
+        return ring16 ? (float)ring16[k] * (1.0f / 32768.0f) : ring[k];
     }
 };
 
@@ -421,7 +422,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
     if (dma) dma_tick(s, 0);
     else load_chunk(0, 0);
     for (;;) {
-    float* ring = g.ring + (int64_t)s * Rs;
+    float* ring = g.ring ? g.ring + (int64_t)s * Rs : nullptr;
+    int16_t* ring16 = g.ring16 ? g.ring16 + (int64_t)s * Rs : nullptr;   // PCM16 pushes only (host-checked)
     GateStream st = g.st[s];
     double* grms = g.block_rms + (int64_t)s * nb;
     double* sorted2 = g.sorted_rms + (int64_t)s * 2 * nb;
@@ -490,7 +492,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
 #pragma unroll
                 for (int m = 0; m < kIngestLoads; ++m) {
                     const int i = c0 + lane + 64 * m;
-                    if (i < fs) {
+                    if (i < fs) {   // (float32 input: never an int16 ring)
                         int k = sp0 + i;
                         if (k >= Rs) k -= Rs;
                         ring[k] = xin[m];
@@ -506,7 +508,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
                 if (i < fs) {
                     int k = sp0 + i;
                     if (k >= Rs) k -= Rs;
-                    ring[k] = xin[m];
+                    if (ring16) ring16[k] = (int16_t)(xin[m] * 32768.0f);   // the PCM16 value, exactly
+                    else ring[k] = xin[m];
                     if (staged) stage[i] = xin[m];
                 }
             }
@@ -534,7 +537,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
                 return pw_sumsq([&](int c0) {
                     int k = (sp0 + (a0 + c0 - p0)) % Rs;
                     if (k < 0) k += Rs;
-                    return RingSrc{ring, k, Rs};
+                    return RingSrc{ring, ring16, k, Rs};
                 }, fs, tbf, tbr, lane, val);
             };
             if (!st.filled && g.compact) {
@@ -634,7 +637,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
                 sum = pw_sumsq([&](int c0) {
                     int f = first + c0;
                     if (f >= Rs) f -= Rs;
-                    return RingSrc{ring, f, Rs};
+                    return RingSrc{ring, ring16, f, Rs};
                 }, nl, tlf, tlr, lane, val);
             }
             const double rms = sqrt(sum / (double)nl);

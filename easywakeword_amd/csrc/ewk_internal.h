@@ -59,6 +59,7 @@ void build_tables64(Tables64* t);
 //   ring  : event i -> ring + stream*ring_len, first sample ring_start, wrap at ring_len
 struct ScoreArgs {
     const float* pcm;
+    const int16_t* pcm16;     // ring mode with an int16 ring (EWK_RING_I16): samples x 32768
     const int64_t* offsets;
     const int32_t* lengths;
     ewk_event* events;        // ring mode: read stream/ring_start/length, write score/match/flags
@@ -114,6 +115,7 @@ hipError_t launch_score_f64(const Tables64* d_tab64, const ScoreArgs& a, int rin
 // (linear) or the ring slice of events[i] (ring_len > 0); output at out[out_offsets[i]].
 struct L3Args {
     const float* pcm;
+    const int16_t* pcm16;        // ring mode with an int16 ring: samples x 32768
     const int64_t* offsets;
     const int32_t* lengths;
     const ewk_event* events;

@@ -45,14 +45,15 @@ __device__ __forceinline__ double l3_leaf_sum(const Src& x, int s, int n) {
 }
 
 struct L3Src {
-    const float* base;   // linear: segment start; ring: stream ring
+    const float* base;   // linear: segment start; ring: stream ring (float32) ...
+    const int16_t* base16;   // ... or int16 ring (EWK_RING_I16): x / 32768, exact
     int32_t start;       // ring: physical index of sample 0
     int32_t ring;        // 0 = linear
     __device__ __forceinline__ double operator()(int i) const {
         if (!ring) return (double)base[i];
         int k = start + i;
         if (k >= ring) k -= ring;
-        return (double)base[k];
+        return base16 ? (double)base16[k] * (1.0 / 32768.0) : (double)base[k];
     }
 };
 
@@ -87,12 +88,14 @@ __global__ __launch_bounds__(64) void k_normalize(L3Args a) {
     int n;
     if (a.ring_len) {
         const ewk_event ev = a.events[i];
-        x.base = a.pcm + (int64_t)ev.stream * a.ring_len;
+        x.base = a.pcm ? a.pcm + (int64_t)ev.stream * a.ring_len : nullptr;
+        x.base16 = a.pcm16 ? a.pcm16 + (int64_t)ev.stream * a.ring_len : nullptr;
         x.start = (int32_t)ev.ring_start;
         x.ring = (int32_t)a.ring_len;
         n = ev.length;
     } else {
         x.base = a.pcm + a.offsets[i];
+        x.base16 = nullptr;
         x.start = 0;
         x.ring = 0;
         n = a.lengths[i];
@@ -103,8 +106,8 @@ __global__ __launch_bounds__(64) void k_normalize(L3Args a) {
     double acc = 0.0;
     for (int c0 = 0; c0 < n; c0 += 8192) {
         const int cn = min(8192, n - c0);
-        const L3Src xc{x.base, x.ring ? (x.start + c0) % x.ring : 0, x.ring};
-        const L3Src xl = x.ring ? xc : L3Src{x.base + c0, 0, 0};
+        const L3Src xc{x.base, x.base16, x.ring ? (x.start + c0) % x.ring : 0, x.ring};
+        const L3Src xl = x.ring ? xc : L3Src{x.base + c0, nullptr, 0, 0};
         for (int k0 = 0; k0 < cn; k0 += 64 * 8) {   // coalesced staging, 8 loads per lane in flight
             float v[8];
 #pragma unroll

@@ -306,6 +306,9 @@ __host__ __device__ constexpr int tr_off(int r, int h) {
 // Segment samples through a buffer descriptor: the hardware range check returns 0
 // outside [0, len) (negative offsets wrap to huge unsigned ones), which is exactly
 // stft(center=True, pad_mode='constant').  Ring segments wrap at the stream ring.
+// RING: 0 linear float32 batch, 1 float32 ring, 2 int16 ring (EWK_RING_I16: the sample
+// is x * 32768; the 1/32768 rides in the window table, a power-of-two scale, so the
+// windowed products are bit-identical to the float32 ring's).
 template <int RING>
 struct SegSrc {
     __amdgpu_buffer_rsrc_t rsrc;   // linear: the segment; ring: the whole stream ring
@@ -315,16 +318,18 @@ struct SegSrc {
     int32_t ring;
 };
 
+constexpr int sample_bytes(int ring) { return ring == 2 ? 2 : 4; }
+
 template <int RING>
-__device__ __forceinline__ SegSrc<RING> make_src(const float* p, int64_t start, int64_t ring, int32_t len) {
+__device__ __forceinline__ SegSrc<RING> make_src(const void* p, int64_t start, int64_t ring, int32_t len) {
     SegSrc<RING> v;
-    const float* b = RING ? p : p + start;
+    const unsigned char* b = static_cast<const unsigned char*>(p) + (RING ? 0 : start * sample_bytes(RING));
     const uint64_t bu = (uint64_t)b;
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)bu);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(bu >> 32));
-    const float* bb = (const float*)(((uint64_t)hi << 32) | lo);
+    const void* bb = (const void*)(((uint64_t)hi << 32) | lo);
     const int32_t n = __builtin_amdgcn_readfirstlane(RING ? (int32_t)ring : len);
-    v.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)bb, (short)0, n * 4, 0x00020000);
+    v.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)bb, (short)0, n * sample_bytes(RING), 0x00020000);
     v.len = __builtin_amdgcn_readfirstlane(len);
     v.start = __builtin_amdgcn_readfirstlane((int32_t)start);
     v.ring = __builtin_amdgcn_readfirstlane((int32_t)ring);
@@ -341,11 +346,14 @@ __device__ __forceinline__ void stage_load(const SegSrc<RING>& v, int q0, int la
         int off;
         if (RING) {
             const int phys = q >= v.wrap_at ? q - v.wrap_at : q + v.start;
-            off = (unsigned)q < (unsigned)v.len ? phys * 4 : -1;
+            off = (unsigned)q < (unsigned)v.len ? phys * sample_bytes(RING) : -1;
         } else {
             off = q * 4;
         }
-        r[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(v.rsrc, off, 0, 0));
+        if (RING == 2)   // buffer_load_sshort + v_cvt_f32_i32: the int16 sample, exactly
+            r[c] = (float)(short)__builtin_amdgcn_raw_buffer_load_b16(v.rsrc, off, 0, 0);
+        else
+            r[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(v.rsrc, off, 0, 0));
     }
 }
 
@@ -1286,10 +1294,12 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, fl
 }
 
 // MODE 0: linear batch; 1: ring events, one segment per workgroup (cooperative); 2: ring
-// events, one segment per wave from the work counter.
-template <int MODE>
+// events, one segment per wave from the work counter.  S16: int16 rings (EWK_RING_I16).
+template <int MODE, int S16>
 __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __restrict__ tab, ScoreArgs a) {
-    constexpr int RING = MODE != 0;
+    constexpr int RING = MODE == 0 ? 0 : (S16 ? 2 : 1);
+    const void* ring_base = S16 ? (const void*)a.pcm16 : (const void*)a.pcm;   // ring modes
+    constexpr float kWinScale = S16 ? 1.0f / 32768.0f : 1.0f;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     // ring mode: the event window and this workgroup's first event, requested before the
     // table fill so their latency overlaps it
@@ -1307,7 +1317,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
         float2* st2 = reinterpret_cast<float2*>(smem + L_TW2);
         for (int i = threadIdx.x; i < 256; i += blockDim.x) {
             const int j = i & 15, n = i >> 4;   // win2[16n + j], tw1[16n + j], tw2[j + 16n]
-            sw2[j * TP + n] = tab->win2[i];
+            sw2[j * TP + n] = make_float2(tab->win2[i].x * kWinScale, tab->win2[i].y * kWinScale);
             if (n > 0) st1[j * TP + n - 1] = tab->tw1[i];
         }
         // [j'][it] = tw2[k] for the bin k that lane class j' untangles at step it
@@ -1393,8 +1403,9 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
             const int seg = base + idx;
             const ewk_event ev = idx == (int)blockIdx.x ? r_ev : a.events[seg];
             if (ev.flags & EWK_EV_SKIPPED) continue;
-            const SegSrc<RING> v = make_src<RING>(a.pcm + (int64_t)ev.stream * a.ring_len, ev.ring_start,
-                                                  a.ring_len, ev.length);
+            const SegSrc<RING> v = make_src<RING>(
+                static_cast<const unsigned char*>(ring_base) + (int64_t)ev.stream * a.ring_len * sample_bytes(RING),
+                ev.ring_start, a.ring_len, ev.length);
             segment_stats_coop(v, smem, scr, tile, tmins, gscr, a.lm_tiles, wave, lane, lo, misc0);
             if (wave == 0 && a.has_template)
                 score_epilogue<RING>(a, act ? misc0[lane] : 0.0f, act ? misc0[20 + lane] : 0.0f, tmf, tsf, lane,
@@ -1410,12 +1421,12 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
         const int seg = base + ((!RING && a.order) ? a.order[idx] : idx);
 
         int64_t start, ring = 0;
-        const float* p;
+        const void* p;
         int32_t len;
         if (RING) {
             const ewk_event ev = a.events[seg];
             if (ev.flags & EWK_EV_SKIPPED) continue;
-            p = a.pcm + (int64_t)ev.stream * a.ring_len;
+            p = static_cast<const unsigned char*>(ring_base) + (int64_t)ev.stream * a.ring_len * sample_bytes(RING);
             start = ev.ring_start;
             ring = a.ring_len;
             len = ev.length;
@@ -1526,10 +1537,11 @@ int score_grid(int n_seg, int ring_mode) {
 hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mode, hipStream_t s) {
     if (a.n_seg <= 0) return hipSuccess;
     const int grid = score_grid(a.n_seg, ring_mode);
-    if (ring_mode == 2) {   // ring mode: the re-score launch re-arms the counter after each tick
-        hipLaunchKernelGGL(k_score_f32<2>, dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
-    } else if (ring_mode) {
-        hipLaunchKernelGGL(k_score_f32<1>, dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
+    if (ring_mode) {   // ring mode: the re-score launch re-arms the counter after each tick
+        if (ring_mode == 2 && a.pcm16) hipLaunchKernelGGL((k_score_f32<2, 1>), dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
+        else if (ring_mode == 2) hipLaunchKernelGGL((k_score_f32<2, 0>), dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
+        else if (a.pcm16) hipLaunchKernelGGL((k_score_f32<1, 1>), dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
+        else hipLaunchKernelGGL((k_score_f32<1, 0>), dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
     } else {
         ScoreArgs b = a;
         // the order only matters once the waves queue several segments each
@@ -1547,7 +1559,7 @@ hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mo
             if (e == hipSuccess && a.rescore_count) e = hipMemsetAsync(a.rescore_count, 0, sizeof(int32_t), s);
             if (e != hipSuccess) return e;
         }
-        hipLaunchKernelGGL(k_score_f32<0>, dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, b);
+        hipLaunchKernelGGL((k_score_f32<0, 0>), dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, b);
     }
     return hipGetLastError();
 }
@@ -1561,7 +1573,8 @@ hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mo
 // ============================================================================
 // numpy's float64 pairwise add.reduce over n strided values (n <= 8192: one ufunc buffer)
 struct SegView {
-    const float* p;   // linear: segment base; ring: stream ring base
+    const float* p;   // linear: segment base; ring: stream ring base (float32) ...
+    const int16_t* p16;   // ... or int16 ring base (EWK_RING_I16)
     int64_t start;    // ring: physical index of sample 0
     int64_t ring;     // 0 = linear
     int32_t len;
@@ -1571,7 +1584,7 @@ __device__ __forceinline__ float seg_sample(const SegView& v, int q) {
     if (q < 0 || q >= v.len) return 0.0f;
     int64_t idx = v.start + q;
     if (v.ring && idx >= v.ring) idx -= v.ring;
-    return v.p[idx];
+    return v.p16 ? (float)v.p16[idx] * (1.0f / 32768.0f) : v.p[idx];
 }
 
 __device__ double pw_sum(const double* a, int n, int stride) {
@@ -1656,12 +1669,14 @@ __device__ __forceinline__ void score_f64_body(const Tables64* __restrict__ tb, 
         SegView v;
         if (RING) {
             const ewk_event ev = a.events[seg];
-            v.p = a.pcm + (int64_t)ev.stream * a.ring_len;
+            v.p = a.pcm ? a.pcm + (int64_t)ev.stream * a.ring_len : nullptr;
+            v.p16 = a.pcm16 ? a.pcm16 + (int64_t)ev.stream * a.ring_len : nullptr;
             v.start = ev.ring_start;
             v.ring = a.ring_len;
             v.len = ev.length;
         } else {
             v.p = a.pcm;
+            v.p16 = nullptr;
             v.start = a.offsets[seg];
             v.ring = 0;
             v.len = a.lengths[seg];

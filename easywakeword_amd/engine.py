@@ -203,7 +203,8 @@ class StreamEngine(Engine):
             raise ValueError("n_streams must be positive")
         super().__init__(gpu=gpu, n_streams=n_streams, config=config, **cfg)
         self.block = int(self.config.block)
-        self.ring_len = int(self.config.buffer_seconds) * FREQUENCY
+        self.ring_len = int(self.config.buffer_seconds) * FREQUENCY          # the reference ring
+        self.sample_ring = int(self.config.ring_samples) or self.ring_len    # samples kept per stream
 
     def push(self, blocks: np.ndarray) -> None:
         """One tick: `blocks` is float32 [n_streams, block] (host)."""
@@ -260,8 +261,14 @@ class StreamEngine(Engine):
         return [out[int(o):int(o) + int(l)] for o, l in zip(offs, lengths)]
 
     def push_device(self, ptr: int, stride: int, tick_stride: int = 0, n_ticks: int = 1) -> None:
+        """Device-resident float32 ticks: stream s, tick t at ptr + 4 * (s * stride + t * tick_stride)."""
         check(self._lib.ewk_push_many(self._h, C.c_void_p(ptr), int(stride), int(tick_stride), int(n_ticks),
                                       _lib.EWK_PUSH_DEVICE))
+
+    def push_device_pcm16(self, ptr: int, stride: int, tick_stride: int = 0, n_ticks: int = 1) -> None:
+        """Device-resident int16 PCM ticks (indexing as push_device, 2-byte samples)."""
+        check(self._lib.ewk_push_many_pcm16(self._h, C.c_void_p(ptr), int(stride), int(tick_stride), int(n_ticks),
+                                            _lib.EWK_PUSH_DEVICE))
 
     def poll(self, cap: Optional[int] = None, lagged: bool = False) -> np.ndarray:
         """Drain queued events as a structured array (see _lib.EVENT_DTYPE).

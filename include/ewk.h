@@ -29,7 +29,7 @@ extern "C" {
 #endif
 
 #define EWK_N_MFCC 20
-#define EWK_ABI_VERSION 2
+#define EWK_ABI_VERSION 3
 
 #define EWK_OK 0
 #define EWK_EINVAL (-1)       /* bad parameter            -> ValueError            */
@@ -47,6 +47,12 @@ extern "C" {
 #define EWK_SCORE_F32_CANDIDATES 2     /* score with the reference's float32-candidate arithmetic
                                           (WordMatcher fed float32 audio); default: float64
                                           candidates, as SoundBuffer slices are (wakeword.py:428) */
+
+/* ewk_config.ring_format */
+#define EWK_RING_F32 0        /* float32 samples (any push)                                  */
+#define EWK_RING_I16 1        /* int16 samples: PCM16 pushes only (ewk_push_pcm16 /
+                                 ewk_push_many_pcm16), stored as delivered -- exact, half the
+                                 HBM per stream; float32 pushes fail with EWK_EINVAL */
 
 /* ewk_push flags */
 #define EWK_PUSH_DEVICE 1     /* pcm is a device pointer */
@@ -81,6 +87,8 @@ typedef struct ewk_config {
     double min_threshold;         /* 0.005  SoundBuffer.MIN_THRESHOLD              */
     double initial_threshold;     /* 0.01   SoundBuffer.silence_threshold init     */
     double rescore_margin;        /* 1e-3   |score - threshold| re-scored in fp64  */
+    int32_t ring_format;          /* EWK_RING_F32 (default) or EWK_RING_I16                    */
+    int32_t reserved1;
 } ewk_config;
 
 /* One level-1 pass (wakeword.py:1097-1124), with its level-2 result. */

@@ -26,7 +26,7 @@ def test_library_exports_every_header_symbol():
 
 def test_struct_layouts_match_header():
     from easywakeword_amd import _lib
-    assert ctypes.sizeof(_lib.EwkConfig) == 4 * 4 + 12 * 8
+    assert ctypes.sizeof(_lib.EwkConfig) == 4 * 4 + 12 * 8 + 2 * 4
     assert ctypes.sizeof(_lib.EwkEvent) == 48
     assert _lib.EVENT_DTYPE.itemsize == 48
 
@@ -39,7 +39,7 @@ def test_defaults_are_reference_constants():
         (0.8, 0.3, 2.0, 0.4)
     assert (c.padding, c.max_segment_seconds, c.similarity_threshold) == (0.05, 3.0, 75.0)
     assert (c.min_threshold, c.initial_threshold, c.tick_seconds) == (0.005, 0.01, 0.1)
-    assert _lib.load().ewk_abi_version() == 2
+    assert _lib.load().ewk_abi_version() == 3
 
 
 def test_no_silent_cpu_fallback():
