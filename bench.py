@@ -481,7 +481,9 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
            "streams_realtime": n_streams * min(1.0, 0.1 / per_tick),
            "gate_kernel_ms_per_tick": gate_ms_tick,
            # the gate's algorithmic bytes: 1600 samples read + written to the ring per stream-tick
-           "gate_hbm_frac": n_streams * 12800 / (gate_ms_tick / 1e3) / (HBM_PEAK_GBS * 1e9) if gate_ms_tick else None,
+           "gate_bytes_per_stream_tick": 2 * 1600 * es,
+           "gate_hbm_frac": n_streams * 2 * 1600 * es / (gate_ms_tick / 1e3) / (HBM_PEAK_GBS * 1e9)
+                            if gate_ms_tick else None,
            "scorer_kernel_ms_per_tick": sc_ms / max(1, sc_n),
            "rescore_kernel_ms_per_tick": r_ms / max(1, r_n),
            "kernel_times": f"separate instrumented pass of {prof_ticks} ticks",

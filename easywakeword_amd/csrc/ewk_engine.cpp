@@ -1162,16 +1162,15 @@ int ewk_read_segment(ewk_engine* e, int32_t stream, int64_t ring_start, int32_t 
     const size_t es = e->ring_es;
     const unsigned char* base = static_cast<const unsigned char*>(e->d_ring) + (size_t)stream * e->sring_len * es;
     const int64_t first = std::min<int64_t>(length, e->sring_len - ring_start);
-    // int16 rings are copied into the tail half of `out` and widened in place (x / 32768, exact)
-    unsigned char* dst = reinterpret_cast<unsigned char*>(out) + (es == sizeof(float) ? 0 : (size_t)length * 2);
+    // int16 rings: copied to a host staging buffer, then widened (x / 32768, exact)
+    std::vector<int16_t> q(es == sizeof(int16_t) ? (size_t)length : 0);
+    unsigned char* dst = es == sizeof(float) ? reinterpret_cast<unsigned char*>(out)
+                                             : reinterpret_cast<unsigned char*>(q.data());
     HIP_TRY(hipMemcpyAsync(dst, base + ring_start * es, first * es, hipMemcpyDeviceToHost, e->stream));
     if (length > first)
         HIP_TRY(hipMemcpyAsync(dst + first * es, base, (length - first) * es, hipMemcpyDeviceToHost, e->stream));
     HIP_TRY(hipStreamSynchronize(e->stream));
-    if (es == sizeof(int16_t)) {
-        const int16_t* q = reinterpret_cast<const int16_t*>(dst);
-        for (int32_t i = 0; i < length; ++i) out[i] = (float)q[i] * (1.0f / 32768.0f);
-    }
+    for (size_t i = 0; i < q.size(); ++i) out[i] = (float)q[i] * (1.0f / 32768.0f);
     return EWK_OK;
 }
 

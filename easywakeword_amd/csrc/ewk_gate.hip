@@ -253,7 +253,9 @@ __device__ __forceinline__ double percentile25_sorted(const double* sorted, int 
 constexpr int kGateWavesPerEU = 4;
 // workgroups of 4 waves: 256 CUs x 16 waves (4 per SIMD); more streams loop inside the waves
 constexpr int kGateGridMax = 1024;
-constexpr int kDma4Chunks = 8;     // 16-B DMA path: ticks of up to 8 * 256 samples copied to the ring in one batch
+constexpr int kDma4Chunks = 8;
+constexpr int kPcm16Pieces = 4;    // int16 path: ticks of up to 4 * 512 samples in 16-B pieces
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));     // 16-B DMA path: ticks of up to 8 * 256 samples copied to the ring in one batch
 constexpr int kIngestLoads = 4;    // tick samples per lane loaded ahead of the ring stores (16: 166 VGPRs, 3 waves/SIMD, 10 % slower)
 
 // ---- register-resident block RMS multiset (n_blocks <= 64 * RB) ------------------
@@ -398,11 +400,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
                                        : __builtin_nontemporal_load(g.pcm + so + i)) : 0.0f;
         }
     };
+    // DMA == 3 (int16 input, block % 8 == 0, 16-B aligned rows): the tick's samples in 16-B
+    // pieces (8 per lane), all in flight at once, widened in registers -- one global round
+    // trip per tick like the float32 LDS-DMA path (the 4-sample chunks above take seven)
+    u32x4 raw[kPcm16Pieces];
+    auto load_vec = [&](int ss, int t) {
+        const int16_t* src = g.pcm16 + (int64_t)ss * g.stride + (int64_t)t * g.tick_stride;
+#pragma unroll
+        for (int c = 0; c < kPcm16Pieces; ++c) {
+            const int i0 = 8 * (lane + 64 * c);
+            raw[c] = i0 < fs ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + i0)) : u32x4{0, 0, 0, 0};
+        }
+    };
     // float32 input with the tick staged in LDS: the tick's samples go global -> LDS by
     // LDS-DMA (global_load_lds), all in flight at once with no VGPRs -- one global round
     // trip per tick instead of one per register chunk
     const bool staged = g.stage >= fs && g.stage >= nl;
-    constexpr bool dma = DMA != 0;   // launch_gate: float32 input, tick and window fit the stage
+    constexpr bool dma = DMA == 1 || DMA == 2;   // launch_gate: float32 input, tick and window fit the stage
     auto dma_tick = [&](int ss, int t) {
         const float* src = g.pcm + (int64_t)ss * g.stride + (int64_t)t * g.tick_stride;
         if (DMA == 2) {   // 16-B pieces (1 KiB per wave-instruction): tick rows 16-B aligned, block % 4 == 0
@@ -420,6 +434,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
         }
     };
     if (dma) dma_tick(s, 0);
+    else if (DMA == 3) load_vec(s, 0);
     else load_chunk(0, 0);
     for (;;) {
     float* ring = g.ring ? g.ring + (int64_t)s * Rs : nullptr;
@@ -500,7 +515,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
                 }
             }
         }
-        for (int c0 = 0; c0 < (dma ? 0 : fs); c0 += 64 * kIngestLoads) {
+        if (DMA == 3) {   // int16 pieces: ring (int16 as delivered, or widened) and stage stores
+#pragma unroll
+            for (int c = 0; c < kPcm16Pieces; ++c) {
+                const int i0 = 8 * (lane + 64 * c);
+                if (i0 < fs) {
+                    int k = sp0 + i0;   // 8-sample groups never straddle the wrap (Rs % 8 == 0)
+                    if (k >= Rs) k -= Rs;
+                    const u32x4 w = raw[c];
+                    float v[8];
+#pragma unroll
+                    for (int h = 0; h < 4; ++h) {
+                        v[2 * h] = (float)(short)(w[h] & 0xffffu) * (1.0f / 32768.0f);
+                        v[2 * h + 1] = (float)((int)w[h] >> 16) * (1.0f / 32768.0f);
+                    }
+                    if (ring16) {
+                        *reinterpret_cast<u32x4*>(ring16 + k) = w;
+                    } else {
+                        *reinterpret_cast<float4*>(ring + k) = make_float4(v[0], v[1], v[2], v[3]);
+                        *reinterpret_cast<float4*>(ring + k + 4) = make_float4(v[4], v[5], v[6], v[7]);
+                    }
+                    if (staged) {
+                        *reinterpret_cast<float4*>(stage + i0) = make_float4(v[0], v[1], v[2], v[3]);
+                        *reinterpret_cast<float4*>(stage + i0 + 4) = make_float4(v[4], v[5], v[6], v[7]);
+                    }
+                }
+            }
+            if (t + 1 < g.n_ticks) load_vec(s, t + 1);   // next tick's samples, in flight during this tick
+        }
+        for (int c0 = 0; c0 < ((dma || DMA == 3) ? 0 : fs); c0 += 64 * kIngestLoads) {
             if (c0 > 0) load_chunk(t, c0);
 #pragma unroll
             for (int m = 0; m < kIngestLoads; ++m) {
@@ -514,7 +557,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
                 }
             }
         }
-        if (t + 1 < g.n_ticks && !dma) load_chunk(t + 1, 0);   // next tick's samples, in flight during this tick
+        if (t + 1 < g.n_ticks && !dma && DMA != 3) load_chunk(t + 1, 0);   // next tick's samples, in flight during this tick
         __threadfence_block();
         wave_sync();
         const bool wrapped = p0 + fs > R;
@@ -735,7 +778,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
     if (lane == 0) g.st[s] = st;
     s += wstride;
     if (s >= g.n_streams) break;
-    if (!dma) load_chunk(0, 0);
+    if (DMA == 3) load_vec(s, 0);
+    else if (!dma) load_chunk(0, 0);
     }
 }
 
@@ -780,12 +824,18 @@ hipError_t launch_gate(const GateArgs& g, hipStream_t s) {
     const bool dma4 = dma && g.block % 4 == 0 && g.block <= 256 * kDma4Chunks &&
                       g.stride % 4 == 0 && g.tick_stride % 4 == 0 && g.ring_len % 4 == 0 && g.sring_len % 4 == 0 &&
                       ((uintptr_t)g.pcm & 15) == 0;
+    // int16 input in 16-B pieces: rows 16-B aligned, whole 8-sample groups
+    const bool vec16 = g.pcm16 != nullptr && g.block % 8 == 0 && g.block <= 512 * kPcm16Pieces &&
+                       g.stride % 8 == 0 && g.tick_stride % 8 == 0 && g.sring_len % 8 == 0 &&
+                       ((uintptr_t)g.pcm16 & 15) == 0;
     if (g.n_blocks <= 128) {
         if (dma4) hipLaunchKernelGGL((k_gate_ticks<2, 2>), dim3(grid), dim3(256), lds, s, g);
+        else if (vec16) hipLaunchKernelGGL((k_gate_ticks<2, 3>), dim3(grid), dim3(256), lds, s, g);
         else if (dma) hipLaunchKernelGGL((k_gate_ticks<2, 1>), dim3(grid), dim3(256), lds, s, g);
         else hipLaunchKernelGGL((k_gate_ticks<2, 0>), dim3(grid), dim3(256), lds, s, g);
     } else if (g.n_blocks <= 64 * kGateRegMax) {
         if (dma4) hipLaunchKernelGGL((k_gate_ticks<kGateRegMax, 2>), dim3(grid), dim3(256), lds, s, g);
+        else if (vec16) hipLaunchKernelGGL((k_gate_ticks<kGateRegMax, 3>), dim3(grid), dim3(256), lds, s, g);
         else if (dma) hipLaunchKernelGGL((k_gate_ticks<kGateRegMax, 1>), dim3(grid), dim3(256), lds, s, g);
         else hipLaunchKernelGGL((k_gate_ticks<kGateRegMax, 0>), dim3(grid), dim3(256), lds, s, g);
     } else {
