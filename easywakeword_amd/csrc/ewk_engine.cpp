@@ -86,7 +86,6 @@ struct ewk_engine {
     DevBuf<int32_t> order;          // linear batches: longest-first work order (k_lpt_order)
     int32_t rescore_cap = 4096;
     DevBuf<double> f64_scratch;
-    DevBuf<float2> lm_scratch;      // parked log-mel tiles + their DCT columns, kLmTiles x 10 KB per scorer wave
     int f64_grid = 64;
 
     // host-API staging
@@ -203,17 +202,6 @@ static hipError_t reserve_rescore(ewk_engine* e, int32_t n_seg) {
     return hipSuccess;
 }
 
-// Size the per-wave log-mel scratch for a launch of `n_seg` segments.
-static hipError_t reserve_lm(ewk_engine* e, int32_t n_seg, int ring_mode) {
-    const size_t waves = (size_t)score_grid(n_seg, ring_mode) * WAVES;
-    const size_t need = waves * kLmTiles * 20 * 64;   // float2 units: 8 KB tile + 2 KB DCT columns
-    if (need <= e->lm_scratch.cap) return hipSuccess;
-    hipError_t err = hipStreamSynchronize(e->stream);
-    if (err == hipSuccess && e->sstream) err = hipStreamSynchronize(e->sstream);
-    if (err != hipSuccess) return err;
-    return e->lm_scratch.reserve(need);
-}
-
 extern "C" {
 
 void ewk_default_config(ewk_config* c) {
@@ -275,7 +263,6 @@ void ewk_destroy(ewk_engine* e) {
     e->rescore_buf.release();
     (void)hipFree(e->d_work);
     e->f64_scratch.release();
-    e->lm_scratch.release();
     e->order.release();
     e->pcm.release();
     e->offsets.release();
@@ -434,7 +421,6 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
         }
         e->ev_cap = std::max(4096, 4 * n_streams);
         if ((err = reserve_rescore(e, e->ev_cap)) != hipSuccess) return bail(err, "rescore list");
-        if ((err = reserve_lm(e, e->ev_cap, 1)) != hipSuccess) return bail(err, "log-mel scratch");
         if ((err = hipMalloc(&e->d_events, 2 * (size_t)e->ev_cap * sizeof(ewk_event))) != hipSuccess)
             return bail(err, "events");
         if ((err = hipMalloc(&e->d_evc, 8 * sizeof(int32_t))) != hipSuccess) return bail(err, "event counters");
@@ -524,8 +510,6 @@ static ScoreArgs base_args(ewk_engine* e) {
     a.rescore_list = e->d_rescore + 1;
     a.rescore_cap = e->rescore_cap;
     a.work = e->d_work;
-    a.lm_scratch = e->lm_scratch.p;
-    a.lm_tiles = kLmTiles;
     a.order = e->order.p;
     return a;
 }
@@ -569,7 +553,6 @@ int ewk_score_segments_device(ewk_engine* e, const float* d_pcm, const int64_t* 
     if (e->has_tmpl && !d_score) return fail(EWK_EINVAL, "d_score is required when a template is set");
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(reserve_rescore(e, n_seg));
-    HIP_TRY(reserve_lm(e, n_seg, 0));
     hipStream_t s = stream ? (hipStream_t)stream : e->stream;
     HIP_TRY(join_scoring(e, s));
     return score_linear(e, d_pcm, d_offsets, d_lengths, n_seg, d_mean, d_std, d_score, d_match, flags, s);
@@ -608,7 +591,6 @@ int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int
         HIP_TRY(e->f64_scratch.reserve((size_t)per * e->f64_grid));
     }
     HIP_TRY(reserve_rescore(e, n_seg));
-    HIP_TRY(reserve_lm(e, n_seg, 0));
     HIP_TRY(e->pcm.reserve(std::max<int64_t>(n_pcm, 1)));
     HIP_TRY(e->offsets.reserve(n_seg));
     HIP_TRY(e->lengths.reserve(n_seg));

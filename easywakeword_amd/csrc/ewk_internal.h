@@ -81,8 +81,6 @@ struct ScoreArgs {
     int32_t* rescore_list;    // indices whose fp32 score fell inside the margin
     int32_t* rescore_count;
     int32_t rescore_cap;
-    float2* lm_scratch;       // per-wave parked log-mel tiles for the top_db clamp pass
-    int32_t lm_tiles;         // tiles per wave in lm_scratch
     int32_t* order;           // linear mode: work order scratch [n_seg] (longest first), nullptr = index order
     // ring mode, k_score_f64: the last workgroup sets *adv_ev_base = *n_events and zeroes
     // *work, *rescore_count (and *adv_done); nullptr = no watermark advance
@@ -104,8 +102,6 @@ hipError_t launch_advance_watermark(int32_t* ev_base, const int32_t* n_events, i
 constexpr int kScoreGridMax = 256;   // one resident workgroup wave of the grid
 constexpr int kScoreGridRing = 256;                     // ring-mode grid (device-side event count)
 int score_grid(int n_seg, int ring_mode);
-// log-mel tiles parked per wave for the top_db pass: segments up to 3 s (T <= 301)
-constexpr int kLmTiles = (1 + 48000 / HOP + 15) / 16;
 // fp64 re-score of rescore_list (device count) or of all n (list == nullptr).
 hipError_t launch_score_f64(const Tables64* d_tab64, const ScoreArgs& a, int ring_mode,
                             double* d_scratch, int64_t scratch_per_seg, int grid,

@@ -33,11 +33,10 @@
 //             splits (Dh Xh + Dh Xl + Dl Xh, f32 accumulation), rows 20..31 zero.
 //   top_db  : power_to_db clamps at (segment max - 80 dB), a segment-global coupling.
 //             Pass 1 clamps each tile speculatively at the running max - 80 dB (exact
-//             once the max is known), parks the stored tile + its DCT columns in a
-//             per-wave global scratch and records the tile minimum; if the segment
-//             min is below the final max - 80 dB, pass 2 revisits only the tiles whose
-//             stored minimum is below it, clamps and swaps their contribution in the
-//             statistics (no second FFT).
+//             once the max is known) and records the stored tile minimum; if the segment
+//             min is below the final max - 80 dB, pass 2 recomputes only the tiles whose
+//             stored minimum is below it and swaps their contribution in the statistics
+//             (nothing is written to global memory but the results).
 //   stats   : population mean/std over frames from fp64 shifted sums
 //             (d = c - c[frame 0]) -- exact 0 std for identical frames.
 //   score   : the reference's own float32 / float64 cosine arithmetic
@@ -104,8 +103,11 @@ constexpr int DCT_RT1_STRIDE = 17 * 16;                   // 16 data chunks [l >
 constexpr int DCT_BYTES = DCT_RT1 + 8 * DCT_RT1_STRIDE;
 constexpr int L_SHARED_END = ((L_DCT + DCT_BYTES) + 15) & ~15;
 constexpr int W_TILE = 0;                                 // 16 frame rows x 512 B of f16 hi/lo chunks (tile_chunk)
-constexpr int W_TMIN = W_TILE + 16 * NMEL * 4;            // per-tile log-mel minima (kLmTiles floats)
-constexpr int W_BYTES = W_TMIN + ((kLmTiles * 4 + 15) & ~15);
+// per-tile record of the speculative top_db clamp (segment_stats): stored log-mel minima,
+// then the clamps (2 x kSpecTiles floats; tiles 0..1023 frames)
+constexpr int kSpecTiles = 64;
+constexpr int W_SPEC = W_TILE + 16 * NMEL * 4;
+constexpr int W_BYTES = W_SPEC + 2 * kSpecTiles * 4;
 constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
 constexpr int LDS_BYTES = L_WG + 16 + 8 * WAVES;
 constexpr int kRescoreFrames = 16;
@@ -124,14 +126,6 @@ __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
         const uint32_t _a = (addr);                                                                \
         EWK_LD128(r, _a, 0); EWK_LD128(r, _a, 1); EWK_LD128(r, _a, 2); EWK_LD128(r, _a, 3);         \
         EWK_LD128(r, _a, 4); EWK_LD128(r, _a, 5); EWK_LD128(r, _a, 6); EWK_LD128(r, _a, 7);         \
-    } while (0)
-#define EWK_LD128S(r, a, c, st) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[c]) : "v"(a), "i"((st) * (c)) : "memory")
-// the 8 KB log-mel tile as float4 [8][64], lane-strided (park copies)
-#define EWK_LD_TILE(r, addr)                                                                               \
-    do {                                                                                                  \
-        const uint32_t _a = (addr);                                                                       \
-        EWK_LD128S(r, _a, 0, 1024); EWK_LD128S(r, _a, 1, 1024); EWK_LD128S(r, _a, 2, 1024); EWK_LD128S(r, _a, 3, 1024); \
-        EWK_LD128S(r, _a, 4, 1024); EWK_LD128S(r, _a, 5, 1024); EWK_LD128S(r, _a, 6, 1024); EWK_LD128S(r, _a, 7, 1024); \
     } while (0)
 #define EWK_WAIT_8(r)                                                                              \
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), \
@@ -260,7 +254,7 @@ __device__ __forceinline__ void split8(const float (&x)[8], uint4& hi, uint4& lo
 // 64 banks.
 __device__ __forceinline__ int tile_chunk(int r, int c) { return 512 * r + 16 * (c ^ r); }
 
-// top_db clamp of a parked tile (its flat 8 KB image `src`): lane l takes the chunk pairs
+// top_db clamp of a log-mel tile (its flat 8 KB LDS image): lane l takes the chunk pairs
 // p = l + 64 u (frame row p >> 4, slot p & 15), rebuilds each value exactly as
 // float(hi) + float(lo), clamps it at theta and writes the re-split pair back in place.
 __device__ __forceinline__ void clamp_load(const float4* src, int lane, uint4 (&h)[4], uint4 (&l)[4]) {
@@ -877,20 +871,66 @@ __device__ __forceinline__ void zero_rows(float* tile, int row0, int lane) {
     for (int m = lane; m < kFPP * NMEL; m += 64) tile[row0 * NMEL + m] = 0.0f;
 }
 
-// Whole segment for one wave.  gscr: this wave's log-mel scratch -- `scr_tiles` flat
-// 16x128-float tiles (float4 [tile][8][64]) followed by the pass-1 DCT columns of each
-// tile (float4 [tile][2][64]); tmins: per-tile log-mel minimum (LDS, one float per tile).
+// The tiles of one segment that pass 1 left holding a value below the final max - 80 dB
+// are recomputed: the stored tile (clamped at its speculative `run`, rebuilt bit for bit
+// by the same frame passes) gives the pass-1 DCT columns to remove, the tile clamped at
+// theta in LDS the columns to add.  (Parking every tile in global memory for this pass
+// instead wrote 10 KB per 16 frames -- 2.3x the algorithmic traffic -- for the ~16 % of
+// bench tiles that need it; recomputing those costs the same time.)
+template <int RING>
+__device__ __forceinline__ void tile_passes(const SegSrc<RING>& v, int tile_i, int T, const unsigned char* smem,
+                                            float* scr, float* tile, int lane, const int (&lo)[8], float& mx,
+                                            float& mn, float clampv) {
+    const int npass = (T + kFPP - 1) / kFPP;
+    {   // stage the tile's first pass
+        float r[kStageLoads];
+        stage_load(v, tile_i * 16 * HOP - NFFT / 2, lane, r);
+        stage_store(scr, lane, r);
+        lds_order();
+    }
+#pragma unroll 1
+    for (int p = 0; p < 16 / kFPP; ++p) {
+        const int pass = tile_i * (16 / kFPP) + p;
+        if (pass < npass)
+            frame_pass(v, pass * kFPP, T, p * kFPP, p + 1 < 16 / kFPP && pass + 1 < npass, smem, scr, tile, lane, lo,
+                       mx, mn, clampv);
+        else   // rows of frames past T: zero (ignored by the statistics)
+            zero_rows(tile, p * kFPP, lane);
+    }
+    lds_order();
+}
+
+template <int RING>
+__device__ __forceinline__ void fix_tile(const SegSrc<RING>& v, int tile_i, int T, float run, float theta,
+                                         const unsigned char* smem, float* scr, float* tile, int lane,
+                                         const int (&lo)[8], const float (&cref)[8], double (&s1)[8],
+                                         double (&s2)[8]) {
+    const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
+    float d0 = 0.f, d1 = 0.f;
+    tile_passes(v, tile_i, T, smem, scr, tile, lane, lo, d0, d1, run);
+    float co[8], cn[8];
+    tile_dct(tile, s_dct, lane, co);
+    {
+        uint4 h[4], l[4];
+        clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
+        clamp_store(tile, lane, h, l, theta);
+    }
+    lds_order();
+    tile_dct(tile, s_dct, lane, cn);
+    stats_replace(cn, co, cref, tile_i * 16 + (lane & 15) < T, s1, s2);
+}
+
+// Whole segment for one wave.  spec: this wave's per-tile record in LDS -- the stored
+// log-mel minimum of tile i in spec[i], its speculative clamp in spec[kSpecTiles + i]
+// (tiles past kSpecTiles are stored unclamped and always recomputed when theta bites).
 template <int RING>
 __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, float* scr, float* tile,
-                              float* tmins, float4* gscr, int scr_tiles, int lane, const int (&lo)[8],
-                              double (&s1)[8], double (&s2)[8]) {
+                              float* spec, int lane, const int (&lo)[8], double (&s1)[8], double (&s2)[8]) {
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     const int T = 1 + v.len / HOP;
     const int ntile = (T + 15) >> 4;
     const int npass = (T + kFPP - 1) / kFPP;
-    const bool park = ntile <= scr_tiles;
     const int col = lane & 15;
-    float4* gcol = gscr + (int64_t)scr_tiles * 8 * 64;
     float cref[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
@@ -901,14 +941,12 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         stage_store(scr, lane, r);
         lds_order();
     }
-    float4* tile4 = reinterpret_cast<float4*>(tile);
     for (int tile_i = 0; tile_i < ntile; ++tile_i) {
         float tmin = INFINITY;
         // speculative top_db clamp at the running max: the final threshold can only be
         // higher, and max(max(x, run), final) = max(x, final), so a tile stored clamped at
-        // `run` is exact when the segment max is already known and is fixed up from its
-        // parked (partly clamped) copy otherwise
-        const float run = park ? wave_max(vmax) - 80.0f : -INFINITY;
+        // `run` is exact when the segment max is already known, and recomputed otherwise
+        const float run = tile_i < kSpecTiles ? wave_max(vmax) - 80.0f : -INFINITY;
 #pragma unroll 1
         for (int p = 0; p < 16 / kFPP; ++p) {
             const int pass = tile_i * (16 / kFPP) + p;
@@ -919,14 +957,6 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
                 zero_rows(tile, p * kFPP, lane);
         }
         lds_order();
-        if (park) {   // all 8 reads in flight, then the stores
-            float4* dst = gscr + (int64_t)tile_i * 8 * 64 + lane;
-            floatx4 t[8];
-            EWK_LD_TILE(t, (uint32_t)(uintptr_t)(tile4 + lane));
-            EWK_WAIT_8(t);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) dst[k * 64] = make_float4(t[k][0], t[k][1], t[k][2], t[k][3]);
-        }
         float c[8];
         tile_dct(tile, s_dct, lane, c);
         if (tile_i == 0) {
@@ -934,14 +964,9 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
             for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
         }
         stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
-        if (park) {
-            float4* dst = gcol + (int64_t)tile_i * 2 * 64 + lane;
-            dst[0] = make_float4(c[0], c[1], c[2], c[3]);
-            dst[64] = make_float4(c[4], c[5], c[6], c[7]);
-        }
         vmin = fminf(vmin, tmin);
         tmin = fmaxf(wave_min(tmin), run);   // the stored tile's minimum
-        if (lane == 0) tmins[min(tile_i, kLmTiles - 1)] = tmin;   // kLmTiles slots: only the parked path reads them
+        if (lane == 0 && tile_i < kSpecTiles) { spec[tile_i] = tmin; spec[kSpecTiles + tile_i] = run; }
     }
     // wave-wide log-mel max/min
     vmax = wave_max(vmax);
@@ -949,60 +974,11 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     const float theta = vmax - 80.0f;
     if (vmin < theta) {
         lds_order();
-        if (park) {
-            // top_db clamp: only tiles holding a value below max - 80 dB change; swap
-            // their pass-1 contribution for the clamped one (parked log-mel + DCT columns)
-            int cur = 0;
-            while (cur < ntile && !(tmins[cur] < theta)) ++cur;
-            uint4 nh[4], nl[4];
-            float4 no0, no1;
-            if (cur < ntile) {
-                clamp_load(gscr + (int64_t)cur * 512, lane, nh, nl);
-                no0 = gcol[(int64_t)cur * 128 + lane];
-                no1 = gcol[(int64_t)cur * 128 + 64 + lane];
-            }
-            while (cur < ntile) {
-                clamp_store(tile, lane, nh, nl, theta);
-                const float co[8] = {no0.x, no0.y, no0.z, no0.w, no1.x, no1.y, no1.z, no1.w};
-                lds_order();
-                int nxt = cur + 1;
-                while (nxt < ntile && !(tmins[nxt] < theta)) ++nxt;
-                if (nxt < ntile) {   // next clamped tile's loads overlap this tile's MFMAs
-                    clamp_load(gscr + (int64_t)nxt * 512, lane, nh, nl);
-                    no0 = gcol[(int64_t)nxt * 128 + lane];
-                    no1 = gcol[(int64_t)nxt * 128 + 64 + lane];
-                }
-                float cn[8];
-                tile_dct(tile, s_dct, lane, cn);
-                stats_replace(cn, co, cref, cur * 16 + col < T, s1, s2);
-                cur = nxt;
-            }
-        } else {
-            // longer than the scratch: recompute the FFT with the clamp applied per tile
-#pragma unroll
-            for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; }
-            {
-                float r[kStageLoads];
-                stage_load(v, -NFFT / 2, lane, r);
-                stage_store(scr, lane, r);
-                lds_order();
-            }
-            float d0 = 0.f, d1 = 0.f;
-            for (int tile_i = 0; tile_i < ntile; ++tile_i) {
-#pragma unroll 1
-                for (int p = 0; p < 16 / kFPP; ++p) {
-                    const int pass = tile_i * (16 / kFPP) + p;
-                    if (pass < npass)
-                        frame_pass(v, pass * kFPP, T, p * kFPP, pass + 1 < npass, smem, scr, tile, lane, lo, d0, d1,
-                                   theta);
-                    else
-                        zero_rows(tile, p * kFPP, lane);
-                }
-                lds_order();
-                float c[8];
-                tile_dct(tile, s_dct, lane, c);
-                stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
-            }
+        for (int cur = 0; cur < ntile; ++cur) {
+            const bool rec = cur < kSpecTiles;
+            if (rec && !(spec[cur] < theta)) continue;
+            fix_tile(v, cur, T, rec ? spec[kSpecTiles + cur] : -INFINITY, theta, smem, scr, tile, lane, lo, cref, s1,
+                     s2);
         }
     }
     finish_stats(T, cref, s1, s2, lane, reinterpret_cast<double*>(scr));
@@ -1017,54 +993,23 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
 // Leaves mean / std (fp32-rounded) in misc0[0..19], misc0[20..39] (wave 0's scratch).
 template <int RING>
 __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, float* scr, float* tile,
-                                   float* tmins, float4* gscr, int scr_tiles, int wave, int lane,
-                                   const int (&lo)[8], float* misc0) {
+                                   float* spec, int wave, int lane, const int (&lo)[8], float* misc0) {
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     float* wg_mm = reinterpret_cast<float*>(smem + L_WG + 16);   // [WAVES][2] max, min
     const int T = 1 + v.len / HOP;
     const int ntile = (T + 15) >> 4;
-    const int npass = (T + kFPP - 1) / kFPP;
     const int nloc = ntile > wave ? (ntile - wave + WAVES - 1) / WAVES : 0;
-    const bool park = nloc <= scr_tiles;
     const int col = lane & 15;
-    float4* gcol = gscr + (int64_t)scr_tiles * 8 * 64;
-    float4* tile4 = reinterpret_cast<float4*>(tile);
     double s1[8], s2[8];
     float cref[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
     float vmax = -INFINITY, vmin = INFINITY;
-    auto run_tile = [&](int tile_i, float& mx, float& mn, float clampv) {
-        {   // stage the tile's first pass
-            float r[kStageLoads];
-            stage_load(v, tile_i * 16 * HOP - NFFT / 2, lane, r);
-            stage_store(scr, lane, r);
-            lds_order();
-        }
-#pragma unroll 1
-        for (int p = 0; p < 16 / kFPP; ++p) {
-            const int pass = tile_i * (16 / kFPP) + p;
-            if (pass < npass)
-                frame_pass(v, pass * kFPP, T, p * kFPP, p + 1 < 16 / kFPP && pass + 1 < npass, smem, scr, tile, lane,
-                           lo, mx, mn, clampv);
-            else
-                zero_rows(tile, p * kFPP, lane);
-        }
-        lds_order();
-    };
     for (int lt = 0; lt < nloc; ++lt) {
         const int tile_i = wave + WAVES * lt;
         float tmin = INFINITY;
-        const float run = park ? wave_max(vmax) - 80.0f : -INFINITY;   // speculative clamp (segment_stats)
-        run_tile(tile_i, vmax, tmin, run);
-        if (park) {
-            float4* dst = gscr + (int64_t)lt * 8 * 64 + lane;
-            floatx4 t[8];
-            EWK_LD_TILE(t, (uint32_t)(uintptr_t)(tile4 + lane));
-            EWK_WAIT_8(t);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) dst[k * 64] = make_float4(t[k][0], t[k][1], t[k][2], t[k][3]);
-        }
+        const float run = lt < kSpecTiles ? wave_max(vmax) - 80.0f : -INFINITY;   // speculative clamp (segment_stats)
+        tile_passes(v, tile_i, T, smem, scr, tile, lane, lo, vmax, tmin, run);
         float c[8];
         tile_dct(tile, s_dct, lane, c);
         if (lt == 0) {
@@ -1072,14 +1017,9 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
             for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
         }
         stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
-        if (park) {
-            float4* dst = gcol + (int64_t)lt * 2 * 64 + lane;
-            dst[0] = make_float4(c[0], c[1], c[2], c[3]);
-            dst[64] = make_float4(c[4], c[5], c[6], c[7]);
-        }
         vmin = fminf(vmin, tmin);
         tmin = fmaxf(wave_min(tmin), run);
-        if (lane == 0) tmins[min(lt, kLmTiles - 1)] = tmin;
+        if (lane == 0 && lt < kSpecTiles) { spec[lt] = tmin; spec[kSpecTiles + lt] = run; }
     }
     vmax = wave_max(vmax);
     vmin = wave_min(vmin);
@@ -1090,33 +1030,11 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
     const float theta = vmax - 80.0f;
     if (vmin < theta && nloc > 0) {
         lds_order();
-        if (park) {
-            for (int lt = 0; lt < nloc; ++lt) {
-                if (!(tmins[lt] < theta)) continue;
-                const int tile_i = wave + WAVES * lt;
-                {
-                    uint4 nh[4], nl[4];
-                    clamp_load(gscr + (int64_t)lt * 512, lane, nh, nl);
-                    clamp_store(tile, lane, nh, nl, theta);
-                }
-                const float4 o0 = gcol[(int64_t)lt * 128 + lane], o1 = gcol[(int64_t)lt * 128 + 64 + lane];
-                const float co[8] = {o0.x, o0.y, o0.z, o0.w, o1.x, o1.y, o1.z, o1.w};
-                lds_order();
-                float cn[8];
-                tile_dct(tile, s_dct, lane, cn);
-                stats_replace(cn, co, cref, tile_i * 16 + col < T, s1, s2);
-            }
-        } else {   // more tiles than the scratch holds: recompute them with the clamp
-#pragma unroll
-            for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; }
-            for (int lt = 0; lt < nloc; ++lt) {
-                const int tile_i = wave + WAVES * lt;
-                float d0 = 0.f, d1 = 0.f;
-                run_tile(tile_i, d0, d1, theta);
-                float c[8];
-                tile_dct(tile, s_dct, lane, c);
-                stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
-            }
+        for (int lt = 0; lt < nloc; ++lt) {
+            const bool rec = lt < kSpecTiles;
+            if (rec && !(spec[lt] < theta)) continue;
+            fix_tile(v, wave + WAVES * lt, T, rec ? spec[kSpecTiles + lt] : -INFINITY, theta, smem, scr, tile, lane, lo,
+                     cref, s1, s2);
         }
     }
     // this wave's per-coefficient (s1, s2, cref) -> its scratch, as doubles [coef][3]
@@ -1374,8 +1292,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
     unsigned char* wbase = smem + L_SHARED_END + wave * W_BYTES;
     float* scr = reinterpret_cast<float*>(smem + L_SCR + wave * SCR_BYTES);
     float* tile = reinterpret_cast<float*>(wbase + W_TILE);
-    float4* gscr = reinterpret_cast<float4*>(a.lm_scratch) + (int64_t)(blockIdx.x * WAVES + wave) * a.lm_tiles * 10 * 64;
-    float* tmins = reinterpret_cast<float*>(wbase + W_TMIN);
+    float* spec = reinterpret_cast<float*>(wbase + W_SPEC);
     int lo[8];   // first bin of this lane's bands j + 16 i
     {
         const int* sb = reinterpret_cast<const int*>(smem + L_BLO);
@@ -1406,7 +1323,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
             const SegSrc<RING> v = make_src<RING>(
                 static_cast<const unsigned char*>(ring_base) + (int64_t)ev.stream * a.ring_len * sample_bytes(RING),
                 ev.ring_start, a.ring_len, ev.length);
-            segment_stats_coop(v, smem, scr, tile, tmins, gscr, a.lm_tiles, wave, lane, lo, misc0);
+            segment_stats_coop(v, smem, scr, tile, spec, wave, lane, lo, misc0);
             if (wave == 0 && a.has_template)
                 score_epilogue<RING>(a, act ? misc0[lane] : 0.0f, act ? misc0[20 + lane] : 0.0f, tmf, tsf, lane,
                                      seg, v.len);
@@ -1438,7 +1355,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
         const SegSrc<RING> v = make_src<RING>(p, start, ring, len);
 
         double st1[8], st2[8];
-        segment_stats(v, smem, scr, tile, tmins, gscr, a.lm_tiles, lane, lo, st1, st2);
+        segment_stats(v, smem, scr, tile, spec, lane, lo, st1, st2);
 
         // ---- lane k < 20 holds coefficient k's mean / std (fp32-rounded like the reference's)
         const float cmf = act ? (float)st1[0] : 0.0f, csf = act ? (float)st2[0] : 0.0f;

@@ -76,7 +76,7 @@ def main():
               f"write {write / 1e9:.3f} GB, total {(fetch + write) / 1e9:.3f} GB")
         print(f"algorithmic bytes per launch (640 B/frame): {alg / 1e9:.3f} GB; "
               f"traffic/algorithmic = {(fetch + write) / alg:.2f}")
-        print(f"  (write = parked log-mel tiles + DCT columns for the top_db pass; their re-read is in fetch)")
+        print(f"  (fetch = segment samples, incl. the re-read of the tiles the top_db pass recomputes; write = results)")
         if len(sys.argv) > 3:
             import json
             with open(sys.argv[3], "w") as fh:
