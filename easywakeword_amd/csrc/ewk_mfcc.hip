@@ -104,10 +104,10 @@ constexpr int DCT_BYTES = DCT_RT1 + 8 * DCT_RT1_STRIDE;
 constexpr int L_SHARED_END = ((L_DCT + DCT_BYTES) + 15) & ~15;
 constexpr int W_TILE = 0;                                 // 16 frame rows x 512 B of f16 hi/lo chunks (tile_chunk)
 // per-tile record of the speculative top_db clamp (segment_stats): stored log-mel minima,
-// then the clamps (2 x kSpecTiles floats; tiles 0..1023 frames)
+// the clamps and the processing order (3 x kSpecTiles; tiles of frames 0..1023)
 constexpr int kSpecTiles = 64;
 constexpr int W_SPEC = W_TILE + 16 * NMEL * 4;
-constexpr int W_BYTES = W_SPEC + 2 * kSpecTiles * 4;
+constexpr int W_BYTES = W_SPEC + 3 * kSpecTiles * 4;     // + the tile order (segment_stats)
 constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
 constexpr int LDS_BYTES = L_WG + 16 + 8 * WAVES;
 constexpr int kRescoreFrames = 16;
@@ -388,13 +388,13 @@ constexpr int kMelOff[8] = {0, 2, 4, 8, 12, 16, 24, 36};
 constexpr int kMelRow = 48;
 static_assert(kMelRow <= WP && WP % 4 == 0, "mel weight rows");
 
-// One 4-frame pass: frames t0 + (lane>>4), samples already staged in `scr`.
-// Writes rows [row0, row0+4) of the log-mel tile (invalid frames -> 0) and
-// returns the per-lane max/min of the valid log-mel values.  If `next` is
-// set, the next pass's samples are fetched meanwhile and staged at the end.
+// One kFPP-frame pass: frames t0 .. t0 + kFPP - 1, samples already staged in `scr`.
+// Writes rows [row0, row0 + kFPP) of the log-mel tile (clamped at clampv) and returns the
+// per-lane max/min of the valid (unclamped) log-mel values.  If next_t0 >= 0, the samples
+// of the pass starting at frame next_t0 are fetched meanwhile and staged at the end.
 // `lo[i]` = first bin of band j + 16 i (per lane, loaded once per kernel).
 template <int RING>
-__device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T, int row0, bool next,
+__device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T, int row0, int next_t0,
                                            const unsigned char* smem, float* scr, float* tile,
                                            int lane, const int (&lo)[8], float& vmax, float& vmin,
                                            float clampv = -INFINITY) {
@@ -623,7 +623,7 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     }
     lds_order();
     EWK_SETPRIO(1);
-    if (next) stage_load(v, (t0 + kFPP) * HOP - NFFT / 2, lane, pf);
+    if (next_t0 >= 0) stage_load(v, next_t0 * HOP - NFFT / 2, lane, pf);
     // ---- mel + log: lane j computes bands m = j + 16*i of its frames (weights shared).
     // The stage's LDS reads go in two batches (band groups 0-5, then 6-7: 19 and 21
     // weights), each followed by its FMAs -- one wait per batch, not one per group.
@@ -693,7 +693,7 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
         *reinterpret_cast<uint4*>(tb + 256) = lo;
     }
     lds_order();
-    if (next) stage_store(scr, lane, pf);
+    if (next_t0 >= 0) stage_store(scr, lane, pf);
     lds_order();
 }
 
@@ -827,6 +827,18 @@ __device__ __forceinline__ double wave_sum_d(double x) {
     return t;
 }
 
+// Sum of a float over the wave (DPP row scans, the row totals via readlane); uniform result.
+__device__ __forceinline__ float wave_sum_f(float x) {
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x111, 0xf, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x112, 0xf, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x114, 0xf, 0xf, false));
+    x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x118, 0xf, 0xf, false));
+    return (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 15)) +
+            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 31))) +
+           (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 47)) +
+            __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 63)));
+}
+
 // Wave maximum of a float (see wave_min).
 __device__ __forceinline__ float wave_max(float x) { return -wave_min(-x); }
 
@@ -892,8 +904,8 @@ __device__ __forceinline__ void tile_passes(const SegSrc<RING>& v, int tile_i, i
     for (int p = 0; p < 16 / kFPP; ++p) {
         const int pass = tile_i * (16 / kFPP) + p;
         if (pass < npass)
-            frame_pass(v, pass * kFPP, T, p * kFPP, p + 1 < 16 / kFPP && pass + 1 < npass, smem, scr, tile, lane, lo,
-                       mx, mn, clampv);
+            frame_pass(v, pass * kFPP, T, p * kFPP, p + 1 < 16 / kFPP && pass + 1 < npass ? (pass + 1) * kFPP : -1,
+                       smem, scr, tile, lane, lo, mx, mn, clampv);
         else   // rows of frames past T: zero (ignored by the statistics)
             zero_rows(tile, p * kFPP, lane);
     }
@@ -920,9 +932,53 @@ __device__ __forceinline__ void fix_tile(const SegSrc<RING>& v, int tile_i, int 
     stats_replace(cn, co, cref, tile_i * 16 + (lane & 15) < T, s1, s2);
 }
 
+// Scout of a segment's tiles (tile t: frames 16t .. 16t + 15): the energy of 4 x 64 of its
+// samples (one 64-sample row every 640), wave-reduced; lane t returns the estimate for tile
+// t (t < ntile <= 64).  Only a processing-order heuristic: the results do not depend on it.
+template <int RING>
+__device__ __forceinline__ float scout_tiles(const SegSrc<RING>& v, int ntile, int lane) {
+    float e = -1.0f;
+    for (int t0 = 0; t0 < ntile; t0 += 4) {
+        float x[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {   // tiles t0 + u (past the segment: range-checked zeros)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int qs = (t0 + u) * 16 * HOP + 640 * q + 64 + lane;
+                int off;
+                if (RING) {
+                    const int phys = qs >= v.wrap_at ? qs - v.wrap_at : qs + v.start;
+                    off = (unsigned)qs < (unsigned)v.len ? phys * sample_bytes(RING) : -1;
+                } else {
+                    off = qs * 4;
+                }
+                if (RING == 2)
+                    x[u][q] = (float)(short)__builtin_amdgcn_raw_buffer_load_b16(v.rsrc, off, 0, 0);
+                else
+                    x[u][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(v.rsrc, off, 0, 0));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float a = x[u][0] * x[u][0];
+#pragma unroll
+            for (int q = 1; q < 4; ++q) a = fmaf(x[u][q], x[u][q], a);
+            const float tot = wave_sum_f(a);
+            if (lane == t0 + u) e = tot;
+        }
+    }
+    return e;
+}
+
 // Whole segment for one wave.  spec: this wave's per-tile record in LDS -- the stored
 // log-mel minimum of tile i in spec[i], its speculative clamp in spec[kSpecTiles + i]
-// (tiles past kSpecTiles are stored unclamped and always recomputed when theta bites).
+// (tiles past kSpecTiles are stored unclamped and always recomputed when theta bites),
+// then the processing order (kSpecTiles ints).
+//
+// The top_db clamp (max - 80 dB over the whole segment) is applied speculatively at the
+// running max, which each tile updates before its DCT; a tile that already holds the
+// segment max needs no fix, so the tiles are processed loudest first by a scout estimate
+// (bench batch: 16 % of the tiles recomputed in time order, ~5 % in scout order).
 template <int RING>
 __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, float* scr, float* tile,
                               float* spec, int lane, const int (&lo)[8], double (&s1)[8], double (&s2)[8]) {
@@ -931,46 +987,70 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     const int ntile = (T + 15) >> 4;
     const int npass = (T + kFPP - 1) / kFPP;
     const int col = lane & 15;
+    int* order = reinterpret_cast<int*>(spec + 2 * kSpecTiles);
+    const bool ordered = ntile > 1 && ntile <= kSpecTiles;
+    if (ordered) {   // loudest-first order: lane t ranks tile t (ties by index)
+        const float e = scout_tiles(v, ntile, lane);
+        int rank = 0;
+        for (int u = 0; u < ntile; ++u) {
+            const float eu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), u));
+            rank += (eu > e) || (eu == e && u < lane);
+        }
+        if (lane < ntile) order[rank] = lane;
+        lds_order();
+    }
     float cref[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
     float vmax = -INFINITY, vmin = INFINITY;
+    int tile_i = ordered ? order[0] : 0;
     {   // stage the first pass synchronously
         float r[kStageLoads];
-        stage_load(v, -NFFT / 2, lane, r);
+        stage_load(v, tile_i * 16 * HOP - NFFT / 2, lane, r);
         stage_store(scr, lane, r);
         lds_order();
     }
-    for (int tile_i = 0; tile_i < ntile; ++tile_i) {
+    float run = -INFINITY;   // speculative clamp: running max - 80 dB
+    for (int k = 0; k < ntile; ++k) {
+        const int next_tile = k + 1 < ntile ? (ordered ? order[k + 1] : k + 1) : -1;
         float tmin = INFINITY;
-        // speculative top_db clamp at the running max: the final threshold can only be
-        // higher, and max(max(x, run), final) = max(x, final), so a tile stored clamped at
-        // `run` is exact when the segment max is already known, and recomputed otherwise
-        const float run = tile_i < kSpecTiles ? wave_max(vmax) - 80.0f : -INFINITY;
+        if (tile_i >= kSpecTiles) run = -INFINITY;
 #pragma unroll 1
         for (int p = 0; p < 16 / kFPP; ++p) {
             const int pass = tile_i * (16 / kFPP) + p;
+            // the next pass to prefetch: this tile's next, else the next tile's first
+            const int nxt = p + 1 < 16 / kFPP && pass + 1 < npass ? (pass + 1) * kFPP
+                                                                  : (next_tile >= 0 ? next_tile * 16 : -1);
             if (pass < npass)
-                frame_pass(v, pass * kFPP, T, p * kFPP, pass + 1 < npass, smem, scr, tile, lane, lo, vmax, tmin,
-                           run);
+                frame_pass(v, pass * kFPP, T, p * kFPP, nxt, smem, scr, tile, lane, lo, vmax, tmin, run);
             else   // rows of frames past T: zero (ignored by the statistics)
                 zero_rows(tile, p * kFPP, lane);
         }
         lds_order();
+        // max(max(x, run), final) = max(x, final): a tile stored clamped at the running max
+        // (this tile's own values included) is exact unless a later tile raises the max
+        const float run2 = tile_i < kSpecTiles ? wave_max(vmax) - 80.0f : -INFINITY;
+        float tmw = wave_min(tmin);
+        if (run2 > run && tmw < run2) {   // this tile raised the max over some of its own values
+            uint4 h[4], l[4];
+            clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
+            clamp_store(tile, lane, h, l, run2);
+            lds_order();
+        }
+        run = fmaxf(run, run2);
         float c[8];
         tile_dct(tile, s_dct, lane, c);
-        if (tile_i == 0) {
+        if (k == 0) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
         }
         stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
-        vmin = fminf(vmin, tmin);
-        tmin = fmaxf(wave_min(tmin), run);   // the stored tile's minimum
-        if (lane == 0 && tile_i < kSpecTiles) { spec[tile_i] = tmin; spec[kSpecTiles + tile_i] = run; }
+        vmin = fminf(vmin, tmw);
+        if (lane == 0 && tile_i < kSpecTiles) { spec[tile_i] = fmaxf(tmw, run); spec[kSpecTiles + tile_i] = run; }
+        tile_i = next_tile;
     }
-    // wave-wide log-mel max/min
+    // wave-wide log-mel max
     vmax = wave_max(vmax);
-    vmin = wave_min(vmin);
     const float theta = vmax - 80.0f;
     if (vmin < theta) {
         lds_order();

@@ -1,0 +1,10 @@
+#!/bin/bash
+# GPU tests of the in-tree library, then the interleaved scorer A/B over variants/*.so
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+TESTS=${1:-tests}
+timeout -k 10 900 python -u -m pytest $TESTS -q -m gpu -x -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest rc=$?"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+timeout -k 10 600 scripts/ab.sh 65536 ${2:-3} > gpurun_out/ab.log 2>&1 || { cat gpurun_out/ab.log; exit 1; }
+cat gpurun_out/ab.log
