@@ -108,9 +108,13 @@ struct ewk_engine {
     GateStream* d_st = nullptr;
     // Two event banks (ev_cap events + 4 counters each: [0] count, [1] dropped,
     // [2] scored watermark): pushes append to `bank`; ewk_poll_lagged drains the
-    // other bank while the GPU still works on this one.
+    // other bank while the GPU still works on this one.  The counters only grow (wrapping
+    // uint32): a drained bank is re-armed by moving its epoch base to the count the host
+    // read -- event i of an epoch is at slot count - base -- so no fill launch per tick.
     ewk_event* d_events = nullptr;   // [2][ev_cap]
     int32_t* d_evc = nullptr;        // [2][4]
+    uint32_t ev_base0[2] = {0, 0};   // per bank: count at the start of the current epoch
+    uint32_t drop_base0[2] = {0, 0}; // per bank: dropped count at the start of the epoch
     int32_t ev_cap = 0;
     int bank = 0;
     bool bank_used[2] = {false, false};
@@ -176,6 +180,8 @@ struct ProfScope {
 
 static void zero_event_state(ewk_engine* e) {
     if (e->d_evc) (void)hipMemsetAsync(e->d_evc, 0, 8 * sizeof(int32_t), e->stream);
+    e->ev_base0[0] = e->ev_base0[1] = 0;
+    e->drop_base0[0] = e->drop_base0[1] = 0;
     e->bank_used[0] = e->bank_used[1] = false;
 }
 
@@ -725,6 +731,7 @@ static int score_pending(ewk_engine* e, hipStream_t ss, const int32_t* n_events)
     a.events = e->ev_bank(e->bank);
     a.n_events = n_events;
     a.ev_base = e->evc_bank(e->bank) + 2;
+    a.ev_base0 = e->ev_base0[e->bank];
     a.n_seg = e->ev_cap;
     a.work = e->d_work + 1;            // ring-mode counters (zeroed at create, re-armed by k_advance)
     a.rescore_count = e->d_work + 2;
@@ -825,6 +832,7 @@ static int push_impl(ewk_engine* e, const void* pcm_any, int64_t stride, int64_t
         g.ev_count = e->evc_bank(e->bank);
         g.ev_dropped = e->evc_bank(e->bank) + 1;
         g.ev_cap = e->ev_cap;
+        g.ev_base0 = e->ev_base0[e->bank];
         const int k = (int)(e->push_seq & 1);
         // the scoring pass two launches back must be done: it read snapshot slot k, and
         // at most one pass runs beside a gate
@@ -990,6 +998,7 @@ constexpr size_t kPollRegion = 16 + (size_t)kPollChunk * sizeof(ewk_event);
 struct BankPeek {
     int32_t n = 0;         // queued events (<= ev_cap)
     int32_t dropped = 0;   // events lost to a full bank
+    uint32_t count = 0, dropped_total = 0;   // the raw counters (the next epoch's bases)
     bool used = false;
 };
 
@@ -1005,15 +1014,19 @@ static int peek_bank(ewk_engine* e, int b, BankPeek* pk) {
     HIP_TRY(hipMemcpyAsync(reg + 16, e->ev_bank(b), (size_t)chunk * sizeof(ewk_event), hipMemcpyDeviceToHost,
                            e->cstream));
     HIP_TRY(hipStreamSynchronize(e->cstream));
-    pk->n = std::min(cnt[0], e->ev_cap);
-    pk->dropped = cnt[1];
+    pk->count = (uint32_t)cnt[0];
+    pk->dropped_total = (uint32_t)cnt[1];
+    pk->n = (int32_t)std::min<uint32_t>(pk->count - e->ev_base0[b], (uint32_t)e->ev_cap);
+    pk->dropped = (int32_t)(pk->dropped_total - e->drop_base0[b]);
     pk->used = true;
     return EWK_OK;
 }
 
-// Re-arm bank b (stream-ordered before any later push into it).
-static int rearm_bank(ewk_engine* e, int b) {
-    HIP_TRY(hipMemsetAsync(e->evc_bank(b), 0, 4 * sizeof(int32_t), e->stream));
+// Re-arm bank b: its next epoch starts at the counters the host just read (no device work;
+// the scorer's watermark is at or behind the new base and is clamped to it).
+static int rearm_bank(ewk_engine* e, int b, const BankPeek& pk) {
+    e->ev_base0[b] = pk.count;
+    e->drop_base0[b] = pk.dropped_total;
     e->bank_used[b] = false;
     return EWK_OK;
 }
@@ -1029,7 +1042,7 @@ static int take_bank(ewk_engine* e, int b, const BankPeek& pk, ewk_event* out) {
             HIP_TRY(hipStreamSynchronize(e->cstream));
         }
     }
-    return rearm_bank(e, b);
+    return rearm_bank(e, b, pk);
 }
 
 // An overflowed bank cannot be delivered whole: re-arm it (its events are lost, the
@@ -1039,7 +1052,7 @@ static int overflow(ewk_engine* e, const BankPeek* pk, const int* banks, int nb)
     for (int i = 0; i < nb; ++i)
         if (pk[i].used && pk[i].dropped > 0) {
             lost += (int64_t)pk[i].n + pk[i].dropped;
-            int rc = rearm_bank(e, banks[i]);
+            int rc = rearm_bank(e, banks[i], pk[i]);
             if (rc) return rc;
         }
     return fail(EWK_ENOMEM, "event queue overflow: " + std::to_string(lost) +

@@ -87,6 +87,7 @@ struct GateArgs {
     int32_t* ev_count;
     int32_t* ev_dropped;
     int32_t ev_cap;
+    int32_t ev_base0;         // the bank's epoch base: event slot = count - ev_base0 (wrapping)
 };
 
 hipError_t launch_gate(const GateArgs& g, hipStream_t s);

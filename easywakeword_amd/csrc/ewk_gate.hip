@@ -753,8 +753,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
                         ev.score = __builtin_nan("");
                         ev.match = 0;
                         ev.flags = ((double)stop / (double)g.sample_rate > g.max_segment_seconds) ? EWK_EV_SKIPPED : 0;
-                        const int slot = atomicAdd(g.ev_count, 1);
-                        if (slot < g.ev_cap) g.events[slot] = ev;
+                        const uint32_t slot = (uint32_t)atomicAdd(g.ev_count, 1) - (uint32_t)g.ev_base0;
+                        if (slot < (uint32_t)g.ev_cap) g.events[slot] = ev;
                         else atomicAdd(g.ev_dropped, 1);
                         st.state = kWaiting;
                     }

@@ -64,7 +64,8 @@ struct ScoreArgs {
     const int32_t* lengths;
     ewk_event* events;        // ring mode: read stream/ring_start/length, write score/match/flags
     const int32_t* n_events;  // ring mode: device-side event count
-    const int32_t* ev_base;   // ring mode: first unscored event (watermark)
+    const int32_t* ev_base;   // ring mode: first unscored event (watermark, count space)
+    int32_t ev_base0;         // ring mode: the bank's epoch base (event slot = count - ev_base0, wrapping)
     int32_t* work;            // per-launch work counter (zeroed before the launch)
     int64_t ring_len;
     int32_t n_seg;            // linear mode count, ring mode capacity

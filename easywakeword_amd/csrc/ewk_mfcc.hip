@@ -1085,11 +1085,28 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
     float vmax = -INFINITY, vmin = INFINITY;
+    // the wave's last tile stays in LDS (unclamped) until the segment max is known, so a
+    // segment of <= WAVES tiles (T <= 128) is never recomputed; earlier tiles are clamped
+    // speculatively at the running max (segment_stats) and recomputed if theta bites
+    float run = -INFINITY, last_min = INFINITY;
     for (int lt = 0; lt < nloc; ++lt) {
         const int tile_i = wave + WAVES * lt;
+        const bool last = lt + 1 == nloc;
+        const bool rec = !last && lt < kSpecTiles;
+        if (!rec) run = -INFINITY;
         float tmin = INFINITY;
-        const float run = lt < kSpecTiles ? wave_max(vmax) - 80.0f : -INFINITY;   // speculative clamp (segment_stats)
         tile_passes(v, tile_i, T, smem, scr, tile, lane, lo, vmax, tmin, run);
+        const float tmw = wave_min(tmin);
+        vmin = fminf(vmin, tmw);
+        if (last) { last_min = tmw; break; }
+        const float run2 = rec ? wave_max(vmax) - 80.0f : -INFINITY;
+        if (run2 > run && tmw < run2) {   // self-clamp (segment_stats)
+            uint4 h[4], l[4];
+            clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
+            clamp_store(tile, lane, h, l, run2);
+            lds_order();
+        }
+        run = fmaxf(run, run2);
         float c[8];
         tile_dct(tile, s_dct, lane, c);
         if (lt == 0) {
@@ -1097,24 +1114,37 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
             for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
         }
         stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
-        vmin = fminf(vmin, tmin);
-        tmin = fmaxf(wave_min(tmin), run);
-        if (lane == 0 && lt < kSpecTiles) { spec[lt] = tmin; spec[kSpecTiles + lt] = run; }
+        if (lane == 0 && rec) { spec[lt] = fmaxf(tmw, run); spec[kSpecTiles + lt] = run; }
     }
     vmax = wave_max(vmax);
-    vmin = wave_min(vmin);
     if (lane == 0) { wg_mm[2 * wave] = vmax; wg_mm[2 * wave + 1] = vmin; }
     __syncthreads();
 #pragma unroll
     for (int w = 0; w < WAVES; ++w) { vmax = fmaxf(vmax, wg_mm[2 * w]); vmin = fminf(vmin, wg_mm[2 * w + 1]); }
     const float theta = vmax - 80.0f;
-    if (vmin < theta && nloc > 0) {
-        lds_order();
-        for (int lt = 0; lt < nloc; ++lt) {
-            const bool rec = lt < kSpecTiles;
-            if (rec && !(spec[lt] < theta)) continue;
-            fix_tile(v, wave + WAVES * lt, T, rec ? spec[kSpecTiles + lt] : -INFINITY, theta, smem, scr, tile, lane, lo,
-                     cref, s1, s2);
+    if (nloc > 0) {
+        const int tile_l = wave + WAVES * (nloc - 1);
+        if (last_min < theta) {   // the last tile, still in LDS: clamp at the final threshold
+            uint4 h[4], l[4];
+            clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
+            clamp_store(tile, lane, h, l, theta);
+            lds_order();
+        }
+        float c[8];
+        tile_dct(tile, s_dct, lane, c);
+        if (nloc == 1) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
+        }
+        stats_add(c, cref, tile_l * 16 + col < T, s1, s2);
+        if (vmin < theta) {
+            lds_order();
+            for (int lt = 0; lt + 1 < nloc; ++lt) {
+                const bool rec = lt < kSpecTiles;
+                if (rec && !(spec[lt] < theta)) continue;
+                fix_tile(v, wave + WAVES * lt, T, rec ? spec[kSpecTiles + lt] : -INFINITY, theta, smem, scr, tile,
+                         lane, lo, cref, s1, s2);
+            }
         }
     }
     // this wave's per-coefficient (s1, s2, cref) -> its scratch, as doubles [coef][3]
@@ -1304,9 +1334,14 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
     int r_base = 0, r_count = 0;
     ewk_event r_ev = {};
     if (RING) {
-        r_base = *a.ev_base;
-        r_count = min(*a.n_events, a.n_seg) - r_base;
+        // counters in wrapping count space; slots relative to the bank's epoch base (a watermark
+        // left behind an epoch -- no template while its events arrived -- restarts at slot 0)
+        r_base = max(0, (int)((uint32_t)*a.ev_base - (uint32_t)a.ev_base0));
+        r_count = min((int)((uint32_t)*a.n_events - (uint32_t)a.ev_base0), a.n_seg) - r_base;
         if ((int)blockIdx.x < r_count) r_ev = a.events[r_base + blockIdx.x];
+        // one segment per workgroup: a workgroup without one skips the table fill (most of
+        // a quiet tick's 256 workgroups)
+        if (MODE == 1 && (int)blockIdx.x >= r_count) return;
     }
     // ---- cooperative table load (global -> LDS), per-lane rows transposed
     {
@@ -1392,21 +1427,24 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
     if (MODE == 1) {
         int* wg_idx = reinterpret_cast<int*>(smem + L_WG);
         float* misc0 = reinterpret_cast<float*>(smem + L_SCR);   // wave 0's FFT scratch (epilogue only)
-        (void)wg_idx;
-        // static assignment (a tick's few hundred segments are about one per workgroup);
-        // the first event was requested before the table fill
-        for (int idx = blockIdx.x; idx < count; idx += gridDim.x) {
-            __syncthreads();   // wave 0's scratch (misc0) is free again
+        // first segment by workgroup index (its event was requested before the table fill),
+        // later ones from the work counter (a burst tick's segments balance over the grid)
+        for (int idx = blockIdx.x; idx < count;) {
+            __syncthreads();   // wave 0's scratch (misc0) and wg_idx are free again
             const int seg = base + idx;
             const ewk_event ev = idx == (int)blockIdx.x ? r_ev : a.events[seg];
-            if (ev.flags & EWK_EV_SKIPPED) continue;
-            const SegSrc<RING> v = make_src<RING>(
-                static_cast<const unsigned char*>(ring_base) + (int64_t)ev.stream * a.ring_len * sample_bytes(RING),
-                ev.ring_start, a.ring_len, ev.length);
-            segment_stats_coop(v, smem, scr, tile, spec, wave, lane, lo, misc0);
-            if (wave == 0 && a.has_template)
-                score_epilogue<RING>(a, act ? misc0[lane] : 0.0f, act ? misc0[20 + lane] : 0.0f, tmf, tsf, lane,
-                                     seg, v.len);
+            if (!(ev.flags & EWK_EV_SKIPPED)) {
+                const SegSrc<RING> v = make_src<RING>(
+                    static_cast<const unsigned char*>(ring_base) + (int64_t)ev.stream * a.ring_len * sample_bytes(RING),
+                    ev.ring_start, a.ring_len, ev.length);
+                segment_stats_coop(v, smem, scr, tile, spec, wave, lane, lo, misc0);
+                if (wave == 0 && a.has_template)
+                    score_epilogue<RING>(a, act ? misc0[lane] : 0.0f, act ? misc0[20 + lane] : 0.0f, tmf, tsf, lane,
+                                         seg, v.len);
+            }
+            if (threadIdx.x == 0) wg_idx[0] = (int)gridDim.x + atomicAdd(a.work, 1);
+            __syncthreads();
+            idx = wg_idx[0];
         }
         return;
     }
@@ -1779,7 +1817,7 @@ __global__ __launch_bounds__(256) void k_score_f64(const Tables64* __restrict__ 
     __shared__ double s_stat[2 * NMFCC];
     int count;
     if (a.rescore_list) count = min(*a.rescore_count, a.rescore_cap);
-    else count = RING ? min(a.n_seg, *a.n_events) : a.n_seg;
+    else count = RING ? min(a.n_seg, (int)((uint32_t)*a.n_events - (uint32_t)a.ev_base0)) : a.n_seg;
     if ((int)blockIdx.x < count) score_f64_body<RING>(tb, a, scratch, per_seg, out_mean64, out_std64, count,
                                                         s_z, s_p, s_win, s_tw, s_cs, s_dct, s_mw, s_mlo, s_moff,
                                                         s_red, s_stat);
