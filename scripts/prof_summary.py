@@ -23,7 +23,7 @@ def main():
         print(f"{short(r['Name']):72s} {int(r['Calls']):6d} {int(r['TotalDurationNs']) / 1e6:10.3f} "
               f"{float(r['AverageNs']) / 1e3:10.1f} {float(r['Percentage']):6.2f}")
     tr = [r for r in csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv")))
-          if "k_score_f32<0>" in r["Kernel_Name"]]
+          if "k_score_f32<0," in r["Kernel_Name"]]
     full = max(int(r["Grid_Size_X"]) for r in tr) if tr else 0
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in tr if int(r["Grid_Size_X"]) == full]
     print(f"\nk_score_f32<0> bench-shaped dispatches (grid {full}): " + ", ".join(f"{x:.3f}" for x in durs) + " ms")
