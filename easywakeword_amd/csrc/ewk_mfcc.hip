@@ -60,8 +60,7 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 // Frames per wave pass: kNF per 16-lane group (kNF = 2: two independent FFTs per lane).
 constexpr int kFPP = 4 * kNF;
 constexpr int kStageLoads = ((kFPP - 1) * HOP + NFFT + 63) / 64;   // dword loads per lane per pass
-// frame fr's FFT scratch starts at fr * 272 + 8 * (fr >> 2): the two frames a 16-lane
-// group untangles side by side (fr, fr + 4) land 8 banks apart
+// frame fr's FFT scratch starts at scr_frame_off(fr) (ewk_internal.h)
 constexpr int kScrFrames = kFPP * SCR_FRAME + 8 * (kNF - 1);
 // kNF = 2: a lane's two frames are consecutive (slot (g, f) = frame 2f + g of the pass),
 // so the second frame's first 11 sample pairs are the first frame's pairs 5..15 (hop 160 =
@@ -406,13 +405,13 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     // rowB = 16 - j' (8 for j' = 0) of frame 4h + f (scratch scf)
     const int jp = j & 7;
     const int rowA = jp, rowB = jp ? 16 - jp : 8;
-    float* scf = scr + (4 * (j >> 3) + f) * SCR_FRAME + 8 * (j >> 3);
+    float* scf = scr + scr_frame_off(4 * (j >> 3) + f);
     bool valid[kNF];
     float* sc[kNF];
 #pragma unroll
     for (int g = 0; g < kNF; ++g) {
         valid[g] = t0 + 2 * f + g < T;
-        sc[g] = scr + (4 * g + f) * SCR_FRAME + 8 * g;
+        sc[g] = scr + scr_frame_off(4 * g + f);
     }
 
     // ---- window the staged samples: lane j holds z[16*n1 + j] = x[32*n1+2j] + i x[32*n1+2j+1]

@@ -81,6 +81,58 @@ static void dct_rows(double* d /* [20][128] */) {
     }
 }
 
+// Per-band read shifts of the mel stage.  Lane (f, j) of a scorer wave reads bins
+// band_lo[j + 16 i] + q (q < group width) of frame 4 g + f for band group i, one ds_read_b32
+// per (g, i, q); the 32 lanes of a half-wave (two frames, 16 bands) collide whenever two
+// addresses share a bank.  A band narrower than its group width may start its read window
+// up to (width - band width) bins early (the extra leading weights are zero: acc + 0 * p =
+// acc, so the sums are bit-identical); the shifts are chosen band by band to minimise the
+// worst bank multiplicity, then the sum of squared multiplicities (simulated LDS cycles of the
+// stage: 296 -> 176 per wave pass, 160 conflict free).
+static int melread_cost(const int* lo_s, int i, int width, long* sq) {
+    int worst_total = 0;
+    for (int g = 0; g < kNF; ++g)
+        for (int q = 0; q < width; ++q)
+            for (int h = 0; h < 2; ++h) {   // half-wave: frames 4 g + 2 h, 4 g + 2 h + 1
+                int addr[32], worst = 0;
+                for (int l = 0; l < 32; ++l) {
+                    const int f = 2 * h + (l >> 4), j = l & 15;
+                    addr[l] = scr_frame_off(4 * g + f) + lo_s[j + 16 * i] + q;
+                }
+                for (int b = 0; b < 64; ++b) {
+                    int distinct[32], nd = 0;
+                    for (int l = 0; l < 32; ++l) {
+                        if (((addr[l] % 64) + 64) % 64 != b) continue;
+                        bool seen = false;
+                        for (int d = 0; d < nd; ++d) seen = seen || distinct[d] == addr[l];
+                        if (!seen) distinct[nd++] = addr[l];
+                    }
+                    worst = nd > worst ? nd : worst;
+                    *sq += (long)nd * nd;
+                }
+                worst_total += worst;
+            }
+    return worst_total;
+}
+
+static void mel_read_shifts(const int* lo, const int* n, const int* gw, int* shift) {
+    int lo_s[NMEL];
+    for (int m = 0; m < NMEL; ++m) { shift[m] = 0; lo_s[m] = lo[m]; }
+    for (int m = 0; m < NMEL; ++m) {
+        const int i = m / 16, slack = gw[i] - n[m];
+        int best_s = 0, best_w = 1 << 30;
+        long best_q = 0;
+        for (int s = 0; s <= slack && lo[m] - s >= 0; ++s) {
+            lo_s[m] = lo[m] - s;
+            long sq = 0;
+            const int w = melread_cost(lo_s, i, gw[i], &sq);
+            if (w < best_w || (w == best_w && sq < best_q)) { best_w = w; best_q = sq; best_s = s; }
+        }
+        shift[m] = best_s;
+        lo_s[m] = lo[m] - best_s;
+    }
+}
+
 void build_tables(Tables* t) {
     memset(t, 0, sizeof(*t));
     double w[NFFT];
@@ -102,6 +154,7 @@ void build_tables(Tables* t) {
     int acc = 0;
     for (int i = 0; i < 8; ++i) { it0[i] = acc; acc += kGroupW[i]; }
     t->ok = acc == MEL_ITERS;
+    int blo[NMEL], bn[NMEL], shift[NMEL];
     for (int m = 0; m < NMEL; ++m) {
         int lo = -1, hi = -1;
         for (int k = 0; k < NBIN; ++k)
@@ -110,12 +163,16 @@ void build_tables(Tables* t) {
                 hi = k;
             }
         if (lo < 0) { lo = 0; hi = -1; }
-        const int n = hi - lo + 1;
-        const int i = m / 16, j = m % 16;
-        if (n > kGroupW[i] || lo + kGroupW[i] > SCR_FRAME) t->ok = 0;
-        t->band_lo[m] = lo;
+        blo[m] = lo;
+        bn[m] = hi - lo + 1;
+        if (bn[m] > kGroupW[m / 16] || lo + kGroupW[m / 16] > SCR_FRAME) t->ok = 0;
+    }
+    mel_read_shifts(blo, bn, kGroupW, shift);
+    for (int m = 0; m < NMEL; ++m) {
+        const int i = m / 16, j = m % 16, s = shift[m];
+        t->band_lo[m] = blo[m] - s;   // the lane's read window starts s bins early
         for (int q = 0; q < kGroupW[i]; ++q)
-            t->wpad[(it0[i] + q) * 16 + j] = q < n ? 0.25f * mel[m * NBIN + lo + q] : 0.0f;
+            t->wpad[(it0[i] + q) * 16 + j] = q >= s && q - s < bn[m] ? 0.25f * mel[m * NBIN + blo[m] + q - s] : 0.0f;
     }
     double d[NMFCC * NMEL];
     dct_rows(d);
