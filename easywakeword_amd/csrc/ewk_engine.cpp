@@ -540,9 +540,10 @@ static int score_linear(ewk_engine* e, const float* d_pcm, const int64_t* d_off,
         HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));
     }
     if (a.has_template) {
-        const int64_t per = (1 + e->ring_len / HOP) * (NMEL + NMFCC);
+        a.f64_scratch = e->f64_scratch.p;
+        a.f64_per_seg = (1 + e->ring_len / HOP) * (NMEL + NMFCC);
         ProfScope ps(e, 1, s);
-        HIP_TRY(launch_score_f64(e->d_tab64, a, 0, e->f64_scratch.p, per, e->f64_grid, nullptr, nullptr, s));
+        HIP_TRY(launch_score_f64(e->d_tab64, a, e->f64_grid, nullptr, nullptr, s));
     }
     return EWK_OK;
 }
@@ -624,7 +625,9 @@ int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int
         HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));   // (zeroes the work counter and the re-score count)
         if (a.has_template) {
             const int64_t tmax = std::max<int64_t>(1 + e->ring_len / HOP, 1 + max_len / HOP);
-            HIP_TRY(launch_score_f64(e->d_tab64, a, 0, e->f64_scratch.p, tmax * (NMEL + NMFCC), e->f64_grid,
+            a.f64_scratch = e->f64_scratch.p;
+            a.f64_per_seg = tmax * (NMEL + NMFCC);
+            HIP_TRY(launch_score_f64(e->d_tab64, a, e->f64_grid,
                                      nullptr, nullptr, s));
         }
     }
@@ -673,7 +676,9 @@ int ewk_score_segments_f64(ewk_engine* e, const float* pcm, int64_t n_pcm, const
     a.cand_f32 = (flags & EWK_SCORE_F32_CANDIDATES) ? 1 : 0;
     a.rescore_list = nullptr;
     a.rescore_count = nullptr;
-    HIP_TRY(launch_score_f64(e->d_tab64, a, 0, e->f64_scratch.p, per, e->f64_grid, e->mean64.p, e->std64.p, s));
+    a.f64_scratch = e->f64_scratch.p;
+    a.f64_per_seg = per;
+    HIP_TRY(launch_score_f64(e->d_tab64, a, e->f64_grid, e->mean64.p, e->std64.p, s));
     if (out_mean) HIP_TRY(hipMemcpyAsync(out_mean, e->mean64.p, (size_t)n_seg * NMFCC * 8, hipMemcpyDeviceToHost, s));
     if (out_std) HIP_TRY(hipMemcpyAsync(out_std, e->std64.p, (size_t)n_seg * NMFCC * 8, hipMemcpyDeviceToHost, s));
     if (out_score && e->has_tmpl)
@@ -733,22 +738,19 @@ static int score_pending(ewk_engine* e, hipStream_t ss, const int32_t* n_events)
     a.ev_base = e->evc_bank(e->bank) + 2;
     a.ev_base0 = e->ev_base0[e->bank];
     a.n_seg = e->ev_cap;
-    a.work = e->d_work + 1;            // ring-mode counters (zeroed at create, re-armed by k_advance)
+    a.work = e->d_work + 1;            // ring-mode counters (zeroed at create, re-armed by the tick end)
     a.rescore_count = e->d_work + 2;
+    // the last workgroup re-scores the near-threshold list in fp64 and advances the watermark
+    // (no second launch per tick)
+    a.adv_done = e->d_work + 3;
+    a.adv_ev_base = e->evc_bank(e->bank) + 2;
+    a.tab64 = e->d_tab64;
+    a.f64_scratch = e->f64_scratch.p;
+    a.f64_per_seg = (1 + e->sring_len / HOP) * (NMEL + NMFCC);
     {
         ProfScope ps(e, 0, ss);
         HIP_TRY(launch_score_f32(e->d_tab, a, e->n_streams >= kRingWaveStreams ? 2 : 1, ss));
     }
-    const int64_t per = (1 + e->sring_len / HOP) * (NMEL + NMFCC);
-    {
-        ProfScope ps(e, 1, ss);
-        // the re-score launch also advances the watermark (its last workgroup: k_advance folded in)
-        a.adv_done = e->d_work + 3;
-        a.adv_ev_base = e->evc_bank(e->bank) + 2;
-        HIP_TRY(launch_score_f64(e->d_tab64, a, 1, e->f64_scratch.p, per, e->f64_grid, nullptr, nullptr, ss));
-    }
-    if (e->f64_grid <= 0)
-        HIP_TRY(launch_advance_watermark(e->evc_bank(e->bank) + 2, n_events, e->d_work + 1, e->d_work + 2, ss));
     return EWK_OK;
 }
 

@@ -86,10 +86,13 @@ struct ScoreArgs {
     int32_t* rescore_count;
     int32_t rescore_cap;
     int32_t* order;           // linear mode: work order scratch [n_seg] (longest first), nullptr = index order
-    // ring mode, k_score_f64: the last workgroup sets *adv_ev_base = *n_events and zeroes
-    // *work, *rescore_count (and *adv_done); nullptr = no watermark advance
+    // ring mode: the last k_score_f32 workgroup out re-scores the listed segments in fp64,
+    // sets *adv_ev_base = *n_events and zeroes *work, *rescore_count and *adv_done
     int32_t* adv_done;
     int32_t* adv_ev_base;
+    const struct Tables64* tab64;   // fp64 re-score tables
+    double* f64_scratch;      // fp64 re-score: [slot][f64_per_seg] log-mel + mfcc rows
+    int64_t f64_per_seg;
 };
 
 // ring_mode: 0 linear batch, 1 ring events one segment per workgroup, 2 ring events one
@@ -99,17 +102,15 @@ hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mo
 constexpr int kRingWaveStreams = 65536;
 // ScoreArgs::order holds n_seg indices followed by kLptScratch ints of bucket counters
 constexpr int kLptScratch = 128;
-// ring mode: *ev_base = *n_events after a scoring pass; zero the ring-mode work counter and re-score count
 hipError_t launch_snapshot(const int32_t* src, int32_t* dst, hipStream_t s);   // *dst = *src, stream-ordered
-hipError_t launch_advance_watermark(int32_t* ev_base, const int32_t* n_events, int32_t* work,
-                                    int32_t* rescore_count, hipStream_t s);
+
 constexpr int kScoreGridMax = 256;   // one resident workgroup wave of the grid
 constexpr int kScoreGridRing = 256;                     // ring-mode grid (device-side event count)
 int score_grid(int n_seg, int ring_mode);
 // fp64 re-score of rescore_list (device count) or of all n (list == nullptr).
-hipError_t launch_score_f64(const Tables64* d_tab64, const ScoreArgs& a, int ring_mode,
-                            double* d_scratch, int64_t scratch_per_seg, int grid,
-                            double* out_mean64, double* out_std64, hipStream_t s);
+// (linear batches; ring ticks re-score inside k_score_f32's last workgroup)
+hipError_t launch_score_f64(const Tables64* d_tab64, const ScoreArgs& a, int grid, double* out_mean64,
+                            double* out_std64, hipStream_t s);
 
 // Level-3 pre-processing (ewk_level3.hip): segment i is pcm[offsets[i] ...][:lengths[i]]
 // (linear) or the ring slice of events[i] (ring_len > 0); output at out[out_offsets[i]].

@@ -1289,7 +1289,7 @@ __device__ __forceinline__ double score_f32_finish(float uu_m, float uu_s, float
 // decision and queues the segment for the fp64 re-score when it is near the threshold.
 template <int RING>
 __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, float csf, float tmf, float tsf,
-                                               int lane, int seg, int len) {
+                                               int lane, int seg, int len, bool& listed) {
     double score;
     if (a.cand_f32) {   // float32 candidates: float products, float-rounded dots (sdot)
         const float uv_m = (float)wave_sum_d((double)(tmf * cmf)), vv_m = (float)wave_sum_d((double)(cmf * cmf));
@@ -1316,9 +1316,83 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, fl
         if (near && a.rescore_list) {
             const int slot = atomicAdd(a.rescore_count, 1);
             if (slot < a.rescore_cap) a.rescore_list[slot] = seg;
+            listed = true;   // (lane 0) this wave queued a segment for the fp64 re-score
         }
     }
 }
+
+// LDS of the fp64 re-score (k_score_f64's static arrays, or carved from k_score_f32's
+// dynamic LDS in the ring-mode tick end)
+struct F64Lds {
+    double2* z;      // [NW][256]
+    double* p;       // [NW][NBIN + 3]
+    double* win;     // [NFFT]
+    double2* tw;     // [128]
+    double2* cs;     // [NBIN]
+    double* dct;     // [NMFCC * NMEL]
+    float* mw;       // [2 * NBIN + 2 * NMEL]
+    int* mlo;        // [NMEL]
+    int* moff;       // [NMEL + 1]
+    double* red;     // [NW]
+    double* stat;    // [2 * NMFCC]
+};
+template <int RING, int NW>
+__device__ __forceinline__ void score_f64_body(const Tables64* __restrict__ tb, const ScoreArgs& a, double* lm, double* out_mean64,
+                               double* out_std64, int first, int count, int stride, const F64Lds& L);
+
+// Ring-mode tick end, run by every workgroup of a k_score_f32 ring launch after its last
+// segment: the last workgroup out re-scores the near-threshold list in fp64 (its 8 waves
+// take the frames in turn; the list is short -- usually empty) and advances the event
+// watermark for the next tick.  Writers publish with a device-scope release before their
+// arrival count: only a workgroup that queued a segment has anything the last one reads or
+// overwrites (the list entry, the event's fp32 score), so only such a workgroup pays the
+// device-scope release (an L2 write-back); the count and the list are read with agent-scope
+// atomic loads.  `listed`: lane 0 of a wave that queued a segment.
+template <int RING>
+__device__ void ring_tick_end(const ScoreArgs& a, unsigned char* smem, bool listed) {
+    int* flag = reinterpret_cast<int*>(smem + L_WG);   // [0] last, [1 + wave] listed
+    const int wave = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) flag[1 + wave] = listed;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int any = 0;
+        for (int w = 0; w < WAVES; ++w) any |= flag[1 + w];
+        if (any) __threadfence();
+        flag[0] = __hip_atomic_fetch_add(a.adv_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    int* last = flag;
+    if (!last[0]) return;
+    const int n = a.rescore_list ? min(__hip_atomic_load(a.rescore_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                       a.rescore_cap)
+                                 : 0;
+    if (n > 0) {
+        unsigned char* q = smem;
+        F64Lds L;
+        L.z = reinterpret_cast<double2*>(q);   q += WAVES * 256 * sizeof(double2);
+        L.p = reinterpret_cast<double*>(q);    q += WAVES * (NBIN + 3) * sizeof(double);
+        L.win = reinterpret_cast<double*>(q);  q += NFFT * sizeof(double);
+        L.tw = reinterpret_cast<double2*>(q);  q += 128 * sizeof(double2);
+        L.cs = reinterpret_cast<double2*>(q);  q += NBIN * sizeof(double2);
+        L.dct = reinterpret_cast<double*>(q);  q += NMFCC * NMEL * sizeof(double);
+        L.red = reinterpret_cast<double*>(q);  q += WAVES * sizeof(double);
+        L.stat = reinterpret_cast<double*>(q); q += 2 * NMFCC * sizeof(double);
+        L.mw = reinterpret_cast<float*>(q);    q += (2 * NBIN + 2 * NMEL) * sizeof(float);
+        L.mlo = reinterpret_cast<int*>(q);     q += NMEL * sizeof(int);
+        L.moff = reinterpret_cast<int*>(q);
+        score_f64_body<RING, WAVES>(a.tab64, a, a.f64_scratch, nullptr, nullptr, 0, n, 1, L);
+    }
+    if (threadIdx.x == 0) {
+        *a.adv_ev_base = *a.n_events;
+        *a.work = 0;
+        *a.rescore_count = 0;
+        *a.adv_done = 0;
+        __threadfence();
+    }
+}
+static_assert(WAVES * 256 * 16 + WAVES * (NBIN + 3) * 8 + NFFT * 8 + 128 * 16 + NBIN * 16 + NMFCC * NMEL * 8 +
+                  WAVES * 8 + 2 * NMFCC * 8 + (2 * NBIN + 2 * NMEL) * 4 + (2 * NMEL + 1) * 4 <= L_WG,
+              "the fp64 re-score carve must end below the ring-mode flag");
 
 // MODE 0: linear batch; 1: ring events, one segment per workgroup (cooperative); 2: ring
 // events, one segment per wave from the work counter.  S16: int16 rings (EWK_RING_I16).
@@ -1340,7 +1414,10 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
         if ((int)blockIdx.x < r_count) r_ev = a.events[r_base + blockIdx.x];
         // one segment per workgroup: a workgroup without one skips the table fill (most of
         // a quiet tick's 256 workgroups)
-        if (MODE == 1 && (int)blockIdx.x >= r_count) return;
+        if (MODE == 1 && (int)blockIdx.x >= r_count) {
+            ring_tick_end<RING>(a, smem, false);
+            return;
+        }
     }
     // ---- cooperative table load (global -> LDS), per-lane rows transposed
     {
@@ -1417,6 +1494,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
     // the template is loop-invariant: fetched once, off every segment's critical path.
     // (Reserving the next work item ahead was tried: the tail imbalance costs more.)
     const bool act = lane < NMFCC;
+    bool listed = false;   // lane 0: this wave queued a segment for the fp64 re-score (ring tick end)
     const float tmf = (a.has_template && act) ? a.tmpl[lane] : 0.0f;
     const float tsf = (a.has_template && act) ? a.tmpl[NMFCC + lane] : 0.0f;
     // Ring mode, MODE 1 (a tick of ~10^3-10^4 streams: a few hundred segments, latency
@@ -1439,12 +1517,13 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
                 segment_stats_coop(v, smem, scr, tile, spec, wave, lane, lo, misc0);
                 if (wave == 0 && a.has_template)
                     score_epilogue<RING>(a, act ? misc0[lane] : 0.0f, act ? misc0[20 + lane] : 0.0f, tmf, tsf, lane,
-                                         seg, v.len);
+                                         seg, v.len, listed);
             }
             if (threadIdx.x == 0) wg_idx[0] = (int)gridDim.x + atomicAdd(a.work, 1);
             __syncthreads();
             idx = wg_idx[0];
         }
+        ring_tick_end<RING>(a, smem, listed);
         return;
     }
     for (;;) {
@@ -1480,23 +1559,10 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
             if (a.out_mean) a.out_mean[(int64_t)seg * NMFCC + lane] = cmf;
             if (a.out_std) a.out_std[(int64_t)seg * NMFCC + lane] = csf;
         }
-        if (a.has_template) score_epilogue<RING>(a, cmf, csf, tmf, tsf, lane, seg, v.len);
+        if (a.has_template) score_epilogue<RING>(a, cmf, csf, tmf, tsf, lane, seg, v.len, listed);
         lds_order();
     }   // work loop
-}
-
-// Ring-mode epilogue: advance the scored-event watermark and re-arm the ring-mode
-// work counter and re-score count for the next tick (saves two memsets per tick).
-__global__ void k_advance(int32_t* ev_base, const int32_t* n_events, int32_t* work, int32_t* rescore_count) {
-    *ev_base = *n_events;
-    *work = 0;
-    *rescore_count = 0;
-}
-
-hipError_t launch_advance_watermark(int32_t* ev_base, const int32_t* n_events, int32_t* work,
-                                    int32_t* rescore_count, hipStream_t s) {
-    hipLaunchKernelGGL(k_advance, dim3(1), dim3(1), 0, s, ev_base, n_events, work, rescore_count);
-    return hipGetLastError();
+    if (RING) ring_tick_end<RING>(a, smem, listed);
 }
 
 // Event-count snapshot taken on the gate's stream right after a gate launch: the
@@ -1679,27 +1745,34 @@ __device__ void fft256_f64(double2* z, const double2* tw, int lane) {
 // One 256-thread workgroup per segment; its four waves take the frames in turn (fp64
 // FFT, packed-support mel, log10), then the workgroup clamps at max - 80 dB, runs the
 // fp64 DCT and numpy's pairwise mean / population std.
-template <int RING>
-__device__ __forceinline__ void score_f64_body(const Tables64* __restrict__ tb, const ScoreArgs& a, double* scratch,
-                                               int64_t per_seg, double* out_mean64, double* out_std64, int count,
-                                               double2 (&s_z)[4][256], double (&s_p)[4][NBIN + 3], double (&s_win)[NFFT],
-                                               double2 (&s_tw)[128], double2 (&s_cs)[NBIN], double (&s_dct)[NMFCC * NMEL],
-                                               float (&s_mw)[2 * NBIN + 2 * NMEL], int (&s_mlo)[NMEL],
-                                               int (&s_moff)[NMEL + 1], double (&s_red)[4], double (&s_stat)[2 * NMFCC]) {
+template <int RING, int NW>
+__device__ __forceinline__ void score_f64_body(const Tables64* __restrict__ tb, const ScoreArgs& a, double* lm,
+                                               double* out_mean64, double* out_std64, int first, int count, int stride,
+                                               const F64Lds& L) {
+    constexpr int NT = 64 * NW;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    for (int i = tid; i < NFFT; i += 256) s_win[i] = tb->win[i];
-    for (int i = tid; i < 128; i += 256) s_tw[i] = make_double2(tb->cs[2 * i], -tb->sn[2 * i]);   // W256^i = W512^2i
-    for (int i = tid; i < NBIN; i += 256) s_cs[i] = make_double2(tb->cs[i], tb->sn[i]);
-    for (int i = tid; i < NMFCC * NMEL; i += 256) s_dct[i] = tb->dct[i];
-    for (int i = tid; i < 2 * NBIN + 2 * NMEL; i += 256) s_mw[i] = tb->mel_w[i];
-    for (int i = tid; i < NMEL; i += 256) s_mlo[i] = tb->mel_lo[i];
-    for (int i = tid; i <= NMEL; i += 256) s_moff[i] = tb->mel_off[i];
+    double* s_win = L.win;
+    double2* s_tw = L.tw;
+    double2* s_cs = L.cs;
+    double* s_dct = L.dct;
+    float* s_mw = L.mw;
+    int* s_mlo = L.mlo;
+    int* s_moff = L.moff;
+    double* s_red = L.red;
+    double* s_stat = L.stat;
+    for (int i = tid; i < NFFT; i += NT) s_win[i] = tb->win[i];
+    for (int i = tid; i < 128; i += NT) s_tw[i] = make_double2(tb->cs[2 * i], -tb->sn[2 * i]);   // W256^i = W512^2i
+    for (int i = tid; i < NBIN; i += NT) s_cs[i] = make_double2(tb->cs[i], tb->sn[i]);
+    for (int i = tid; i < NMFCC * NMEL; i += NT) s_dct[i] = tb->dct[i];
+    for (int i = tid; i < 2 * NBIN + 2 * NMEL; i += NT) s_mw[i] = tb->mel_w[i];
+    for (int i = tid; i < NMEL; i += NT) s_mlo[i] = tb->mel_lo[i];
+    for (int i = tid; i <= NMEL; i += NT) s_moff[i] = tb->mel_off[i];
     __syncthreads();
-    double* lm = scratch + (int64_t)blockIdx.x * per_seg;   // [T][128] log-mel, then [T][20] mfcc
-    double2* z = s_z[wave];
-    double* pw = s_p[wave];
-    for (int w = blockIdx.x; w < count; w += gridDim.x) {
-        const int seg = a.rescore_list ? a.rescore_list[w] : w;
+    // lm: this workgroup's [T][128] log-mel, then [T][20] mfcc
+    double2* z = L.z + 256 * wave;
+    double* pw = L.p + (NBIN + 3) * wave;
+    for (int w = first; w < count; w += stride) {
+        const int seg = a.rescore_list ? __hip_atomic_load(a.rescore_list + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : w;
         SegView v;
         if (RING) {
             const ewk_event ev = a.events[seg];
@@ -1716,9 +1789,9 @@ __device__ __forceinline__ void score_f64_body(const Tables64* __restrict__ tb, 
             v.len = a.lengths[seg];
         }
         const int T = 1 + v.len / HOP;
-        if ((int64_t)T * (NMEL + NMFCC) > per_seg) continue;   // host sizes scratch; never expected
+        if ((int64_t)T * (NMEL + NMFCC) > a.f64_per_seg) continue;   // host sizes scratch; never expected
         double lmax = -INFINITY;
-        for (int t = wave; t < T; t += 4) {
+        for (int t = wave; t < T; t += NW) {
             // windowed z[n] = x[2n] + i x[2n+1], stored bit-reversed for the in-place FFT
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -1757,9 +1830,11 @@ __device__ __forceinline__ void score_f64_body(const Tables64* __restrict__ tb, 
         for (int o = 32; o > 0; o >>= 1) lmax = fmax(lmax, __shfl_xor(lmax, o, 64));
         if (lane == 0) s_red[wave] = lmax;
         __syncthreads();
-        const double theta = fmax(fmax(s_red[0], s_red[1]), fmax(s_red[2], s_red[3])) - 80.0;
+        double mx = s_red[0];
+        for (int w2 = 1; w2 < NW; ++w2) mx = fmax(mx, s_red[w2]);
+        const double theta = mx - 80.0;
         double* mf = lm + (int64_t)T * NMEL;
-        for (int i = tid; i < T * NMFCC; i += 256) {
+        for (int i = tid; i < T * NMFCC; i += NT) {
             const int t = i / NMFCC, k = i % NMFCC;
             const double* row = lm + (int64_t)t * NMEL;
             const double* dk = s_dct + k * NMEL;
@@ -1802,7 +1877,6 @@ __device__ __forceinline__ void score_f64_body(const Tables64* __restrict__ tb, 
 
 template <int RING>
 __global__ __launch_bounds__(256) void k_score_f64(const Tables64* __restrict__ tb, ScoreArgs a,
-                                                   double* scratch, int64_t per_seg,
                                                    double* out_mean64, double* out_std64) {
     __shared__ double2 s_z[4][256];
     __shared__ double s_p[4][NBIN + 3];
@@ -1814,38 +1888,18 @@ __global__ __launch_bounds__(256) void k_score_f64(const Tables64* __restrict__ 
     __shared__ int s_mlo[NMEL], s_moff[NMEL + 1];
     __shared__ double s_red[4];
     __shared__ double s_stat[2 * NMFCC];
+    const F64Lds L = {&s_z[0][0], &s_p[0][0], s_win, s_tw, s_cs, s_dct, s_mw, s_mlo, s_moff, s_red, s_stat};
     int count;
     if (a.rescore_list) count = min(*a.rescore_count, a.rescore_cap);
     else count = RING ? min(a.n_seg, (int)((uint32_t)*a.n_events - (uint32_t)a.ev_base0)) : a.n_seg;
-    if ((int)blockIdx.x < count) score_f64_body<RING>(tb, a, scratch, per_seg, out_mean64, out_std64, count,
-                                                        s_z, s_p, s_win, s_tw, s_cs, s_dct, s_mw, s_mlo, s_moff,
-                                                        s_red, s_stat);
-    // ring mode: the last workgroup out advances the watermark and re-arms the counters
-    // (k_advance folded in: one launch fewer per tick)
-    if (a.adv_done) {
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __threadfence();
-            if (atomicAdd(a.adv_done, 1) == (int)gridDim.x - 1) {
-                *a.adv_ev_base = *a.n_events;
-                *a.work = 0;
-                *a.rescore_count = 0;
-                *a.adv_done = 0;
-                __threadfence();
-            }
-        }
-    }
+    if ((int)blockIdx.x < count)
+        score_f64_body<RING, 4>(tb, a, a.f64_scratch + (int64_t)blockIdx.x * a.f64_per_seg, out_mean64, out_std64,
+                                (int)blockIdx.x, count, (int)gridDim.x, L);
 }
-hipError_t launch_score_f64(const Tables64* d_tab64, const ScoreArgs& a, int ring_mode, double* d_scratch,
-                            int64_t scratch_per_seg, int grid, double* out_mean64, double* out_std64,
-                            hipStream_t s) {
+hipError_t launch_score_f64(const Tables64* d_tab64, const ScoreArgs& a, int grid, double* out_mean64,
+                            double* out_std64, hipStream_t s) {
     if (grid <= 0) return hipSuccess;
-    if (ring_mode)
-        hipLaunchKernelGGL(k_score_f64<1>, dim3(grid), dim3(256), 0, s, d_tab64, a, d_scratch, scratch_per_seg,
-                           out_mean64, out_std64);
-    else
-        hipLaunchKernelGGL(k_score_f64<0>, dim3(grid), dim3(256), 0, s, d_tab64, a, d_scratch, scratch_per_seg,
-                           out_mean64, out_std64);
+    hipLaunchKernelGGL(k_score_f64<0>, dim3(grid), dim3(256), 0, s, d_tab64, a, out_mean64, out_std64);
     return hipGetLastError();
 }
 
