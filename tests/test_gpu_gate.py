@@ -109,6 +109,46 @@ def test_many_streams_vs_oracle(template):
     assert n_ev > 20
 
 
+def test_ring_tick_fp64_rescore_in_last_workgroup(template):
+    """rescore_margin = 1e9: every ring segment is queued for the fp64 re-score, which the
+    last k_score_f32 workgroup of the tick runs (no separate launch): all events carry
+    EWK_EV_RESCORED and the float64 reference score within 1e-9, over several ticks per
+    push and several pushes (the watermark advances in the same tick end)."""
+    gate = dict(pre_speech_silence=0.8, speech_duration_min=0.3, speech_duration_max=2.0, post_speech_silence=0.4)
+    n = 12
+    pcms = []
+    for i in range(n):
+        rng = np.random.default_rng(900 + i)
+        p, _ = synth.make_stream(seed=4000 + i, n_words=3, sigma=float(rng.uniform(1e-4, 3e-3)),
+                                 gain=float(rng.uniform(0.3, 2.0)), distractors=bool(i % 2))
+        pcms.append(p)
+    L = min(len(p) for p in pcms)
+    L -= L % 1600
+    data = np.stack([p[:L] for p in pcms]).astype(np.float32)
+    eng = _engine(n, gate, rescore_margin=1e9)
+    eng.set_template(*template)
+    got = []
+    for c in range(0, L, 8 * 1600):
+        eng.push_many(data[:, c:c + 8 * 1600])
+        got.extend(eng.poll().tolist())
+    tm, ts = template
+    n_ev = 0
+    for i in range(n):
+        ref = _oracle_events(data[i], gate)
+        mine = sorted([g for g in got if g[0] == i], key=lambda g: g[2])
+        assert [(g[2], g[1], bool(g[7] & 1)) for g in mine] == [(e.tick, e.length, e.skipped) for e in ref], i
+        for g, e in zip(mine, ref):
+            if e.skipped:
+                continue
+            assert g[7] & 2, (i, g)   # EWK_EV_RESCORED
+            cm, cs = mfcc_ref.extract_mfcc(e.audio)
+            s = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
+            assert score_close(g[5], s, 1e-9), (i, g, s)
+            assert bool(g[6]) == (s >= 75.0)
+            n_ev += 1
+    assert n_ev >= 12
+
+
 def test_unaligned_block_512_thresholds():
     """frame_size 512: 312 physical blocks, the write pointer is not block-aligned
     after the first wrap -> exercises the incremental block-RMS refresh."""
@@ -158,9 +198,9 @@ def test_lagged_poll_pipelines_one_call_behind():
 
 def test_long_segments_cooperative_scorer(template):
     """Segments of 8 s and 26 s through the ring-mode scorer: a workgroup's waves
-    share each segment (7 and 21 tiles per wave: the parked top_db pass and the
-    recompute fallback for more tiles than the per-wave scratch holds), scores
-    vs the oracle."""
+    share each segment (7 and 21 tiles per wave: each wave's last tile waits in LDS
+    for the segment max, earlier ones are clamped speculatively and recomputed when
+    top_db bites), scores vs the oracle."""
     gate = dict(pre_speech_silence=0.8, speech_duration_min=0.3, speech_duration_max=40.0,
                 post_speech_silence=0.4, buffer_seconds=60)
     sr = 16000

@@ -173,11 +173,11 @@ def test_longest_first_order_is_bit_identical(engine):
 
 def test_speculative_top_db_clamp(engine):
     """Pass 1 clamps each 16-frame tile at the running segment max - 80 dB
-    (top_db).  A loud burst placed in the last tile forces
-    every earlier (quiet) tile through the parked fix-up; one in the first tile
-    makes every later tile exact in pass 1; a burst mid-way mixes both.  All must
-    equal the oracle, and a quiet tail after the burst must not be clamped at a
-    stale threshold."""
+    (top_db), the tiles taken loudest first by a sample scout.  A
+    loud burst placed in the last tile, the first tile or mid-way, and a tone in the last
+    0.2 s (a single loud tile the scout must find) -- every quiet tile the threshold bites
+    is either exact in pass 1 or recomputed.  All must equal the oracle, and a quiet tail
+    after the burst must not be clamped at a stale threshold."""
     engine.template_from_pcm(synth.load_word())
     tm, ts = engine.get_template()
     rng = np.random.Generator(np.random.PCG64(5))
@@ -216,3 +216,27 @@ def test_extract_mfcc_keeps_the_input_dtype():
         np.testing.assert_allclose(s64, rs, rtol=0, atol=1e-9 * max(1.0, float(np.abs(rs).max())))
         m32, s32 = m.extract_mfcc(x.astype(np.float32))
         assert m32.dtype == np.float32 and s32.dtype == np.float32
+
+
+def test_top_db_past_the_tile_record(engine):
+    """Segments longer than the per-wave tile record (kSpecTiles = 64 tiles, 1024 frames):
+    taken in time order, the tiles past the record are stored unclamped and always
+    recomputed when top_db bites -- a loud burst early, mid-way or at the end of 12-20 s
+    of quiet noise must still equal the oracle."""
+    engine.template_from_pcm(synth.load_word())
+    tm, ts = engine.get_template()
+    rng = np.random.Generator(np.random.PCG64(8))
+    word = synth.load_word()
+    segs = []
+    for L, where in ((192000, 0.1), (200000, 0.55), (320000, 1.0)):
+        x = rng.normal(0, 1e-5, L).astype(np.float32)
+        w = word * np.float32(2.5)
+        s0 = int(where * (L - len(w)))
+        x[s0:s0 + len(w)] += w
+        segs.append(x)
+    _, _, score, match = engine.score(segs, candidate_dtype="float64")
+    for i, x in enumerate(segs):
+        cm, cs = mfcc_ref.extract_mfcc(x.astype(np.float64))
+        ref = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
+        assert score_close(score[i], ref, SCORE_TOL), (i, len(x), score[i], ref)
+        assert bool(match[i]) == (ref >= 75.0)
