@@ -934,38 +934,45 @@ __device__ __forceinline__ void fix_tile(const SegSrc<RING>& v, int tile_i, int 
 // Scout of a segment's tiles (tile t: frames 16t .. 16t + 15): the energy of 4 x 64 of its
 // samples (one 64-sample row every 640), wave-reduced; lane t returns the estimate for tile
 // t (t < ntile <= 64).  Only a processing-order heuristic: the results do not depend on it.
+template <int RING, int NB>
+__device__ __forceinline__ void scout_batch(const SegSrc<RING>& v, int t0, int lane, float& e) {
+    float x[NB][4];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {   // tiles t0 + u (past the segment: range-checked zeros)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int qs = (t0 + u) * 16 * HOP + 640 * q + 64 + lane;
+            int off;
+            if (RING) {
+                const int phys = qs >= v.wrap_at ? qs - v.wrap_at : qs + v.start;
+                off = (unsigned)qs < (unsigned)v.len ? phys * sample_bytes(RING) : -1;
+            } else {
+                off = qs * 4;
+            }
+            if (RING == 2)
+                x[u][q] = (float)(short)__builtin_amdgcn_raw_buffer_load_b16(v.rsrc, off, 0, 0);
+            else
+                x[u][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(v.rsrc, off, 0, 0));
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        float a = x[u][0] * x[u][0];
+#pragma unroll
+        for (int q = 1; q < 4; ++q) a = fmaf(x[u][q], x[u][q], a);
+        const float tot = wave_sum_f(a);
+        if (lane == t0 + u) e = tot;
+    }
+}
+
+// Scout of a segment's tiles (tile t: frames 16t .. 16t + 15): the energy of 4 x 64 of its
+// samples (one 64-sample row every 640), wave-reduced; lane t returns the estimate for tile
+// t (t < ntile <= 64).  Only a processing-order heuristic: the results do not depend on it.
+// The loads of 8 tiles are in flight together (one memory round trip per 1.3 s of segment).
 template <int RING>
 __device__ __forceinline__ float scout_tiles(const SegSrc<RING>& v, int ntile, int lane) {
     float e = -1.0f;
-    for (int t0 = 0; t0 < ntile; t0 += 4) {
-        float x[4][4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {   // tiles t0 + u (past the segment: range-checked zeros)
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int qs = (t0 + u) * 16 * HOP + 640 * q + 64 + lane;
-                int off;
-                if (RING) {
-                    const int phys = qs >= v.wrap_at ? qs - v.wrap_at : qs + v.start;
-                    off = (unsigned)qs < (unsigned)v.len ? phys * sample_bytes(RING) : -1;
-                } else {
-                    off = qs * 4;
-                }
-                if (RING == 2)
-                    x[u][q] = (float)(short)__builtin_amdgcn_raw_buffer_load_b16(v.rsrc, off, 0, 0);
-                else
-                    x[u][q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(v.rsrc, off, 0, 0));
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            float a = x[u][0] * x[u][0];
-#pragma unroll
-            for (int q = 1; q < 4; ++q) a = fmaf(x[u][q], x[u][q], a);
-            const float tot = wave_sum_f(a);
-            if (lane == t0 + u) e = tot;
-        }
-    }
+    for (int t0 = 0; t0 < ntile; t0 += 8) scout_batch<RING, 8>(v, t0, lane, e);
     return e;
 }
 
