@@ -43,3 +43,11 @@ if [ "$MODE" = all ] || [ "$MODE" = pmcgate ]; then
   rc=$?; echo "pmc gate rc=$rc"; [ $rc -eq 0 ] || exit $rc
   python "$R/scripts/pmc_gate_summary.py" "${EWK_RAW:-$R/gpurun_out}/pmc_gate" 8192 > "$R/gpurun_out/pmc_gate_summary.txt" 2>&1
 fi
+if [ "$MODE" = pmcgatemax ]; then   # the 2,097,152-stream int16 config (the bench's streaming_max)
+  R="${GRAFT_REPO_ROOT:-/root/repo}"
+  EWK_PMC_BENCH_ARGS="--big-streams 0 --stream-count 64" bash "$R/scripts/pmc_gate.sh" gatemax \
+     "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" \
+     "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_INSTS_SMEM GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE"
+  rc=$?; echo "pmc gate max rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  python "$R/scripts/pmc_gate_summary.py" "${EWK_RAW:-$R/gpurun_out}/pmc_gatemax" 2097152 > "$R/gpurun_out/pmc_gatemax_summary.txt" 2>&1
+fi
