@@ -270,17 +270,17 @@ __device__ __forceinline__ double reg_get(const double (&v)[RB], int i) {
 }
 
 template <int RB>
-__device__ __forceinline__ void reg_set(double (&v)[RB], int i, double x, int lane) {
+__device__ __forceinline__ void reg_set(double (&v)[RB], int i, double x, int lane, uint32_t& dirty) {
 #pragma unroll
     for (int j = 0; j < RB; ++j)
-        if ((i >> 6) == j && lane == (i & 63)) v[j] = x;
+        if ((i >> 6) == j && lane == (i & 63)) { v[j] = x; dirty |= 1u << j; }
 }
 
 // so (sorted, nb values) with one occurrence of vo replaced by vn, kept sorted: the
 // new element d comes from old element d - 1, d or d + 1 (or is vn), so the update is
 // two neighbour shuffles.  Returns false when vo is absent (caller re-sorts).
 template <int RB>
-__device__ bool reg_replace(double (&so)[RB], int nb, double vo, double vn, int lane) {
+__device__ bool reg_replace(double (&so)[RB], int nb, double vo, double vn, int lane, uint32_t& dirty) {
     int pos = nb;
 #pragma unroll
     for (int j = RB - 1; j >= 0; --j) {
@@ -317,13 +317,15 @@ __device__ bool reg_replace(double (&so)[RB], int nb, double vo, double vn, int 
         const int i = i1 < pos ? i1 : i1 + 1;
         const double x = i == d ? so[j] : (i < d ? prev[j] : next[j]);
         so[j] = d == cnt ? vn : x;
+        if (d >= min(pos, cnt) && d <= max(pos, cnt)) dirty |= 1u << (RB + j);   // elements that moved
     }
     return true;
 }
 
 // First fill / repair: so = sorted copy of gr (stable rank sort through LDS scratch tmp[nb]).
 template <int RB>
-__device__ void reg_rank_sort(const double (&gr)[RB], double (&so)[RB], int nb, double* tmp, int lane) {
+__device__ void reg_rank_sort(const double (&gr)[RB], double (&so)[RB], int nb, double* tmp, int lane, uint32_t& dirty) {
+    dirty |= ((1u << RB) - 1) << RB;
 #pragma unroll
     for (int j = 0; j < RB; ++j) {
         const int i = lane + 64 * j;
@@ -448,6 +450,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
     const PwTree* tlr = trees + kTreeLastRem;
     constexpr int RBn = RB > 0 ? RB : 1;
     double gr[RBn], srt[RBn];
+    uint32_t dirty = 0;   // register path: bit j = gr[j] changed, bit RB + j = srt[j] changed (stored back only then)
     if (RB > 0) {   // (this path never double-buffers: sorted_sel stays 0)
 #pragma unroll
         for (int j = 0; j < RBn; ++j) {
@@ -588,23 +591,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
                 // are whole ticks); the last one is this tick's, then the first sort
                 const int b = p0 / fs;
                 const double v = sqrt(block_sum(b) / (double)fs);
-                if (RB > 0) reg_set(gr, b, v, lane);
+                if (RB > 0) reg_set(gr, b, v, lane, dirty);
                 else if (lane == 0) grms[b] = v;
                 __threadfence_block();
                 wave_sync();
-                if (RB > 0) reg_rank_sort(gr, srt, nb, val, lane);
+                if (RB > 0) reg_rank_sort(gr, srt, nb, val, lane, dirty);
                 else rank_sort(grms, sorted2, nb, lane);
                 st.sorted_sel = 0;
                 st.filled = 1;
             } else if (!st.filled) {
                 for (int b = 0; b < nb; ++b) {
                     const double sum = block_sum(b);
-                    if (RB > 0) reg_set(gr, b, sqrt(sum / (double)fs), lane);
+                    if (RB > 0) reg_set(gr, b, sqrt(sum / (double)fs), lane, dirty);
                     else if (lane == 0) grms[b] = sqrt(sum / (double)fs);
                 }
                 __threadfence_block();
                 wave_sync();
-                if (RB > 0) reg_rank_sort(gr, srt, nb, val, lane);
+                if (RB > 0) reg_rank_sort(gr, srt, nb, val, lane, dirty);
                 else rank_sort(grms, sorted2, nb, lane);
                 st.sorted_sel = 0;
                 st.filled = 1;
@@ -622,8 +625,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
                         }
                         if (RB > 0) {
                             const double vo = reg_get(gr, b);
-                            reg_set(gr, b, v, lane);
-                            if (!reg_replace(srt, nb, vo, v, lane)) reg_rank_sort(gr, srt, nb, val, lane);
+                            reg_set(gr, b, v, lane, dirty);
+                            if (!reg_replace(srt, nb, vo, v, lane, dirty)) reg_rank_sort(gr, srt, nb, val, lane, dirty);
                             continue;
                         }
                         const double vo = grms[b];
@@ -662,7 +665,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
             const int b = p0 / fs;
             const double v = sqrt(pw_sumsq([&](int c0) { return LdsSrc{stage + c0}; }, fs, tbf, tbr, lane, val) /
                                   (double)fs);
-            if (RB > 0) reg_set(gr, b, v, lane);
+            if (RB > 0) reg_set(gr, b, v, lane, dirty);
             else if (lane == 0) grms[b] = v;
         }
         // ---- a3: is_silent(): RMS of the last n_last samples < threshold
@@ -768,11 +771,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
         st.sound_start = __shfl(st.sound_start, 0, 64);
         st.sound_end = __shfl(st.sound_end, 0, 64);
     }
-    if (RB > 0 && (st.filled || g.compact)) {
+    if (RB > 0 && (st.filled || g.compact)) {   // only the elements this launch changed (one block RMS per tick)
 #pragma unroll
         for (int j = 0; j < RBn; ++j) {
             const int i = lane + 64 * j;
-            if (i < nb) { grms[i] = gr[j]; sorted2[i] = srt[j]; }
+            if (i < nb && (dirty & (1u << j))) grms[i] = gr[j];
+            if (i < nb && (dirty & (1u << (RB + j)))) sorted2[i] = srt[j];
         }
     }
     if (lane == 0) g.st[s] = st;
