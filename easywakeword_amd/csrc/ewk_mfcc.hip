@@ -110,6 +110,7 @@ constexpr int W_BYTES = W_SPEC + 3 * kSpecTiles * 4;     // + the tile order (se
 constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
 constexpr int LDS_BYTES = L_WG + 16 + 8 * WAVES;
 constexpr int kRescoreFrames = 16;
+constexpr double kTinyStd = 2.0;   // |std vector| below which the fp64 path decides (speech: >= 25)
 static_assert(LDS_BYTES <= 160 * 1024, "the workgroup must fit a CU's LDS");
 static_assert(16 % kFPP == 0, "passes must tile the 16-frame log-mel tile");
 
@@ -1297,22 +1298,28 @@ __device__ __forceinline__ double score_f32_finish(float uu_m, float uu_s, float
 template <int RING>
 __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, float csf, float tmf, float tsf,
                                                int lane, int seg, int len, bool& listed) {
-    double score;
+    double score, std2;
     if (a.cand_f32) {   // float32 candidates: float products, float-rounded dots (sdot)
         const float uv_m = (float)wave_sum_d((double)(tmf * cmf)), vv_m = (float)wave_sum_d((double)(cmf * cmf));
         const float uv_s = (float)wave_sum_d((double)(tsf * csf)), vv_s = (float)wave_sum_d((double)(csf * csf));
         score = score_f32_finish(a.uu_m32, a.uu_s32, uv_m, vv_m, uv_s, vv_s);
+        std2 = vv_s;
     } else {
         const double uv_m = wave_sum_d((double)tmf * (double)cmf), vv_m = wave_sum_d((double)cmf * (double)cmf);
         const double uv_s = wave_sum_d((double)tsf * (double)csf), vv_s = wave_sum_d((double)csf * (double)csf);
         score = score_f64_finish((double)a.uu_m32, (double)a.uu_s32, uv_m, vv_m, uv_s, vv_s);
+        std2 = vv_s;
     }
     if (lane == 0) {
         const int match = score >= a.threshold;
-        // fp64 re-score: decisions within the margin of the threshold, and very short
-        // segments (T <= kRescoreFrames) whose 2..16-frame std vectors are too
-        // ill-conditioned for the float32 pipeline to meet 1e-4.
-        const bool near = fabs(score - a.threshold) < a.rescore_margin || (1 + len / HOP) <= kRescoreFrames;
+        // fp64 re-score: decisions within the margin of the threshold; very short segments
+        // (T <= kRescoreFrames) whose 2..16-frame std vectors are too ill-conditioned for the
+        // float32 pipeline to meet 1e-4; and nearly constant segments (0 < |std| < kTinyStd:
+        // a few bins above the -100 dB floor, std vectors ~1e-2..1 whose direction the float32
+        // rounding of the MFCCs (~1e-4 absolute) moves).  An exactly constant segment keeps
+        // its NaN (zero std; the reference's own value there is a rounding artefact).
+        const bool near = fabs(score - a.threshold) < a.rescore_margin || (1 + len / HOP) <= kRescoreFrames ||
+                          (std2 > 0.0 && std2 < kTinyStd * kTinyStd);
         if (RING) {
             a.events[seg].score = score;
             a.events[seg].match = match;
