@@ -49,9 +49,10 @@ if __name__ == "__main__":
     e = ewa.Engine()
     e.template_from_pcm(synth.load_word())
     tm, ts = e.get_template()
-    mean, std, score, match = e.score(segs, candidate_dtype="float64")
+    dt = os.environ.get("FUZZ_DTYPE", "float64")
+    mean, std, score, match = e.score(segs, candidate_dtype=dt)
     for i, x in enumerate(segs):
-        cm, cs = mfcc_ref.extract_mfcc(x.astype(np.float64))
+        cm, cs = mfcc_ref.extract_mfcc(x.astype(np.float64) if dt == "float64" else x.astype(np.float32))
         ref = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
         bad = not (abs(score[i] - ref) < 1e-4 or (np.isnan(score[i]) and np.isnan(ref)))
         print(i, len(x), "gpu %.6f ref %.6f %s" % (score[i], ref, "BAD" if bad else ""),
