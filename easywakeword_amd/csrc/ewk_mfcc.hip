@@ -388,6 +388,41 @@ constexpr int kMelOff[8] = {0, 2, 4, 8, 12, 16, 24, 36};
 constexpr int kMelRow = 48;
 static_assert(kMelRow <= WP && WP % 4 == 0, "mel weight rows");
 
+// Column writes of one frame set's transpose image (one plane: real or imaginary), with
+// ds_write_addtid_b32 (address = M0 + offset + 4 lane).
+template <int G>
+__device__ __forceinline__ void xpose_write(const float2 (&ag)[16], int half, uint32_t m0base) {
+    constexpr int g = G;
+    float w[16];
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) w[k1] = half ? ag[dperm(k1)].y : ag[dperm(k1)].x;
+    // M0 is compiler-reserved: saved and restored in the same statement; the
+    // s_nop covers the M0-write -> LDS-use hazard (without it the stores use the old M0)
+    uint32_t m0save;
+    asm volatile("s_mov_b32 %[sv], m0\n\ts_mov_b32 m0, %[base]\n\ts_nop 0\n\t"
+                 "ds_write_addtid_b32 %[w0] offset:%[o0]\n\tds_write_addtid_b32 %[w1] offset:%[o1]\n\t"
+                 "ds_write_addtid_b32 %[w2] offset:%[o2]\n\tds_write_addtid_b32 %[w3] offset:%[o3]\n\t"
+                 "ds_write_addtid_b32 %[w4] offset:%[o4]\n\tds_write_addtid_b32 %[w5] offset:%[o5]\n\t"
+                 "ds_write_addtid_b32 %[w6] offset:%[o6]\n\tds_write_addtid_b32 %[w7] offset:%[o7]\n\t"
+                 "ds_write_addtid_b32 %[w8] offset:%[o8]\n\tds_write_addtid_b32 %[w9] offset:%[o9]\n\t"
+                 "ds_write_addtid_b32 %[w10] offset:%[o10]\n\tds_write_addtid_b32 %[w11] offset:%[o11]\n\t"
+                 "ds_write_addtid_b32 %[w12] offset:%[o12]\n\tds_write_addtid_b32 %[w13] offset:%[o13]\n\t"
+                 "ds_write_addtid_b32 %[w14] offset:%[o14]\n\tds_write_addtid_b32 %[w15] offset:%[o15]\n\t"
+                 "s_mov_b32 m0, %[sv]"
+                 : [sv] "=&s"(m0save)
+                 : [base] "s"(m0base), [w0] "v"(w[0]), [w1] "v"(w[1]), [w2] "v"(w[2]), [w3] "v"(w[3]),
+                   [w4] "v"(w[4]), [w5] "v"(w[5]), [w6] "v"(w[6]), [w7] "v"(w[7]), [w8] "v"(w[8]),
+                   [w9] "v"(w[9]), [w10] "v"(w[10]), [w11] "v"(w[11]), [w12] "v"(w[12]),
+                   [w13] "v"(w[13]), [w14] "v"(w[14]), [w15] "v"(w[15]),
+                   [o0] "i"(4 * tr_off(0, g)), [o1] "i"(4 * tr_off(1, g)), [o2] "i"(4 * tr_off(2, g)),
+                   [o3] "i"(4 * tr_off(3, g)), [o4] "i"(4 * tr_off(4, g)), [o5] "i"(4 * tr_off(5, g)),
+                   [o6] "i"(4 * tr_off(6, g)), [o7] "i"(4 * tr_off(7, g)), [o8] "i"(4 * tr_off(8, g)),
+                   [o9] "i"(4 * tr_off(9, g)), [o10] "i"(4 * tr_off(10, g)), [o11] "i"(4 * tr_off(11, g)),
+                   [o12] "i"(4 * tr_off(12, g)), [o13] "i"(4 * tr_off(13, g)), [o14] "i"(4 * tr_off(14, g)),
+                   [o15] "i"(4 * tr_off(15, g))
+                 : "memory");
+}
+
 // One kFPP-frame pass: frames t0 .. t0 + kFPP - 1, samples already staged in `scr`.
 // Writes rows [row0, row0 + kFPP) of the log-mel tile (clamped at clampv) and returns the
 // per-lane max/min of the valid (unclamped) log-mel values.  If next_t0 >= 0, the samples
@@ -492,34 +527,8 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
         for (int half = 0; half < 2; ++half) {
 #pragma unroll
             for (int g = 0; g < kNF; ++g) {
-                float w[16];
-#pragma unroll
-                for (int k1 = 0; k1 < 16; ++k1) w[k1] = half ? a[g][dperm(k1)].y : a[g][dperm(k1)].x;
-                // M0 is compiler-reserved: saved and restored in the same statement; the
-                // s_nop covers the M0-write -> LDS-use hazard (without it the stores use the old M0)
-                uint32_t m0save;
-                asm volatile("s_mov_b32 %[sv], m0\n\ts_mov_b32 m0, %[base]\n\ts_nop 0\n\t"
-                             "ds_write_addtid_b32 %[w0] offset:%[o0]\n\tds_write_addtid_b32 %[w1] offset:%[o1]\n\t"
-                             "ds_write_addtid_b32 %[w2] offset:%[o2]\n\tds_write_addtid_b32 %[w3] offset:%[o3]\n\t"
-                             "ds_write_addtid_b32 %[w4] offset:%[o4]\n\tds_write_addtid_b32 %[w5] offset:%[o5]\n\t"
-                             "ds_write_addtid_b32 %[w6] offset:%[o6]\n\tds_write_addtid_b32 %[w7] offset:%[o7]\n\t"
-                             "ds_write_addtid_b32 %[w8] offset:%[o8]\n\tds_write_addtid_b32 %[w9] offset:%[o9]\n\t"
-                             "ds_write_addtid_b32 %[w10] offset:%[o10]\n\tds_write_addtid_b32 %[w11] offset:%[o11]\n\t"
-                             "ds_write_addtid_b32 %[w12] offset:%[o12]\n\tds_write_addtid_b32 %[w13] offset:%[o13]\n\t"
-                             "ds_write_addtid_b32 %[w14] offset:%[o14]\n\tds_write_addtid_b32 %[w15] offset:%[o15]\n\t"
-                             "s_mov_b32 m0, %[sv]"
-                             : [sv] "=&s"(m0save)
-                             : [base] "s"(m0base), [w0] "v"(w[0]), [w1] "v"(w[1]), [w2] "v"(w[2]), [w3] "v"(w[3]),
-                               [w4] "v"(w[4]), [w5] "v"(w[5]), [w6] "v"(w[6]), [w7] "v"(w[7]), [w8] "v"(w[8]),
-                               [w9] "v"(w[9]), [w10] "v"(w[10]), [w11] "v"(w[11]), [w12] "v"(w[12]),
-                               [w13] "v"(w[13]), [w14] "v"(w[14]), [w15] "v"(w[15]),
-                               [o0] "i"(4 * tr_off(0, g)), [o1] "i"(4 * tr_off(1, g)), [o2] "i"(4 * tr_off(2, g)),
-                               [o3] "i"(4 * tr_off(3, g)), [o4] "i"(4 * tr_off(4, g)), [o5] "i"(4 * tr_off(5, g)),
-                               [o6] "i"(4 * tr_off(6, g)), [o7] "i"(4 * tr_off(7, g)), [o8] "i"(4 * tr_off(8, g)),
-                               [o9] "i"(4 * tr_off(9, g)), [o10] "i"(4 * tr_off(10, g)), [o11] "i"(4 * tr_off(11, g)),
-                               [o12] "i"(4 * tr_off(12, g)), [o13] "i"(4 * tr_off(13, g)), [o14] "i"(4 * tr_off(14, g)),
-                               [o15] "i"(4 * tr_off(15, g))
-                             : "memory");
+                if (g == 0) xpose_write<0>(a[0], half, m0base);
+                else xpose_write<1>(a[1], half, m0base);
             }
             lds_order();
             // lane (h, j') = (j >> 3, j & 7) reads two columns of frame 4h + f: c0 = j' and its
