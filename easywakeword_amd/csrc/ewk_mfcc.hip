@@ -431,7 +431,7 @@ __device__ __forceinline__ void xpose_write(const float2 (&ag)[16], int half, ui
 template <int RING>
 __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T, int row0, int next_t0,
                                            const unsigned char* smem, float* scr, float* tile,
-                                           int lane, const int (&lo)[8], float& vmax, float& vmin,
+                                           int lane, const int (&lo)[8], float& vmax, float& vmin, float& nanp,
                                            float clampv = -INFINITY) {
     EWK_SETPRIO(1);
     // lane group f = lane>>4 holds frames fr = 4 g + f (g < kNF) of this pass; the
@@ -674,6 +674,10 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
                     for (int q = 0; q < kMelW[i]; ++q) acc = fmaf(wv[kMelIt0[i] + q], pv[g][kMelIt0[i] + q], acc);
                     // 10*log10(x) = (10*log10(2)) * log2(x), v_log_f32
                     db[g][i] = 3.0102999566398120f * __log2f(fmaxf(1e-10f, acc));
+                    // NaN probe: a NaN sample makes every bin of its frame NaN, which the
+                    // amin floor above would hide (fmax returns the number); the reference's
+                    // np.maximum propagates it and scores NaN (acc * 0 is NaN for NaN / Inf)
+                    if (i == 0) nanp = fmaf(acc, 0.0f, nanp);
                 }
         }
     }
@@ -901,7 +905,7 @@ __device__ __forceinline__ void zero_rows(float* tile, int row0, int lane) {
 template <int RING>
 __device__ __forceinline__ void tile_passes(const SegSrc<RING>& v, int tile_i, int T, const unsigned char* smem,
                                             float* scr, float* tile, int lane, const int (&lo)[8], float& mx,
-                                            float& mn, float clampv) {
+                                            float& mn, float& nanp, float clampv) {
     const int npass = (T + kFPP - 1) / kFPP;
     {   // stage the tile's first pass
         float r[kStageLoads];
@@ -914,7 +918,7 @@ __device__ __forceinline__ void tile_passes(const SegSrc<RING>& v, int tile_i, i
         const int pass = tile_i * (16 / kFPP) + p;
         if (pass < npass)
             frame_pass(v, pass * kFPP, T, p * kFPP, p + 1 < 16 / kFPP && pass + 1 < npass ? (pass + 1) * kFPP : -1,
-                       smem, scr, tile, lane, lo, mx, mn, clampv);
+                       smem, scr, tile, lane, lo, mx, mn, nanp, clampv);
         else   // rows of frames past T: zero (ignored by the statistics)
             zero_rows(tile, p * kFPP, lane);
     }
@@ -927,8 +931,8 @@ __device__ __forceinline__ void fix_tile(const SegSrc<RING>& v, int tile_i, int 
                                          const int (&lo)[8], const float (&cref)[8], double (&s1)[8],
                                          double (&s2)[8]) {
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
-    float d0 = 0.f, d1 = 0.f;
-    tile_passes(v, tile_i, T, smem, scr, tile, lane, lo, d0, d1, run);
+    float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+    tile_passes(v, tile_i, T, smem, scr, tile, lane, lo, d0, d1, d2, run);
     float co[8], cn[8];
     tile_dct(tile, s_dct, lane, co);
     {
@@ -1006,7 +1010,8 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     int* order = reinterpret_cast<int*>(spec + 2 * kSpecTiles);
     const bool ordered = ntile > 1 && ntile <= kSpecTiles;
     if (ordered) {   // loudest-first order: lane t ranks tile t (ties by index)
-        const float e = scout_tiles(v, ntile, lane);
+        float e = scout_tiles(v, ntile, lane);
+        e = e == e ? e : 0.0f;   // NaN samples: a total order (unique ranks) all the same
         int rank = 0;
         for (int u = 0; u < ntile; ++u) {
             const float eu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), u));
@@ -1018,7 +1023,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     float cref[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
-    float vmax = -INFINITY, vmin = INFINITY;
+    float vmax = -INFINITY, vmin = INFINITY, nanp = 0.0f;
     int tile_i = ordered ? order[0] : 0;
     {   // stage the first pass synchronously
         float r[kStageLoads];
@@ -1038,7 +1043,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
             const int nxt = p + 1 < 16 / kFPP && pass + 1 < npass ? (pass + 1) * kFPP
                                                                   : (next_tile >= 0 ? next_tile * 16 : -1);
             if (pass < npass)
-                frame_pass(v, pass * kFPP, T, p * kFPP, nxt, smem, scr, tile, lane, lo, vmax, tmin, run);
+                frame_pass(v, pass * kFPP, T, p * kFPP, nxt, smem, scr, tile, lane, lo, vmax, tmin, nanp, run);
             else   // rows of frames past T: zero (ignored by the statistics)
                 zero_rows(tile, p * kFPP, lane);
         }
@@ -1077,6 +1082,10 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
                      s2);
         }
     }
+    if (__ballot(nanp != nanp)) {   // NaN input: NaN statistics, NaN score (like the reference)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s1[i] = __builtin_nan("");
+    }
     finish_stats(T, cref, s1, s2, lane, reinterpret_cast<double*>(scr));
 }
 
@@ -1100,7 +1109,7 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
     float cref[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
-    float vmax = -INFINITY, vmin = INFINITY;
+    float vmax = -INFINITY, vmin = INFINITY, nanp = 0.0f;
     // the wave's last tile stays in LDS (unclamped) until the segment max is known, so a
     // segment of <= WAVES tiles (T <= 128) is never recomputed; earlier tiles are clamped
     // speculatively at the running max (segment_stats) and recomputed if theta bites
@@ -1111,7 +1120,7 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
         const bool rec = !last && lt < kSpecTiles;
         if (!rec) run = -INFINITY;
         float tmin = INFINITY;
-        tile_passes(v, tile_i, T, smem, scr, tile, lane, lo, vmax, tmin, run);
+        tile_passes(v, tile_i, T, smem, scr, tile, lane, lo, vmax, tmin, nanp, run);
         const float tmw = wave_min(tmin);
         vmin = fminf(vmin, tmw);
         if (last) { last_min = tmw; break; }
@@ -1162,6 +1171,10 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
                          lane, lo, cref, s1, s2);
             }
         }
+    }
+    if (__ballot(nanp != nanp)) {   // NaN input (segment_stats): the combined sums go NaN
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s1[i] = __builtin_nan("");
     }
     // this wave's per-coefficient (s1, s2, cref) -> its scratch, as doubles [coef][3]
     double* pd = reinterpret_cast<double*>(scr);
@@ -1844,7 +1857,7 @@ __device__ __forceinline__ void score_f64_body(const Tables64* __restrict__ tb, 
                 const int lo = s_mlo[m], o0 = s_moff[m], o1 = s_moff[m + 1];
                 double acc = 0.0;
                 for (int o = o0; o < o1; ++o) acc = fma((double)s_mw[o], pw[lo + o - o0], acc);
-                const double db = 10.0 * log10(fmax(1e-10, acc));
+                const double db = 10.0 * log10(acc < 1e-10 ? 1e-10 : acc);   // np.maximum: NaN propagates
                 lm[(int64_t)t * NMEL + m] = db;
                 lmax = fmax(lmax, db);
             }
@@ -1862,7 +1875,7 @@ __device__ __forceinline__ void score_f64_body(const Tables64* __restrict__ tb, 
             const double* row = lm + (int64_t)t * NMEL;
             const double* dk = s_dct + k * NMEL;
             double acc = 0.0;
-            for (int m = 0; m < NMEL; ++m) acc = fma(dk[m], fmax(row[m], theta), acc);
+            for (int m = 0; m < NMEL; ++m) acc = fma(dk[m], row[m] < theta ? theta : row[m], acc);
             mf[i] = acc;
         }
         __syncthreads();

@@ -291,3 +291,30 @@ def test_top_db_order_fuzz(engine):
         assert score_close(score[i], ref, SCORE_TOL), (i, len(x), score[i], ref)
         assert bool(match[i]) == (ref >= 75.0), (i, score[i], ref)
     assert 0 < n_const < 10
+
+
+def test_non_finite_samples_do_not_disturb_the_batch(engine):
+    """NaN / Inf samples (corrupt input) give the reference's NaN score -- librosa propagates
+    them -- without disturbing the other segments of the batch (the scout's ranking and the
+    per-tile record must stay well formed)."""
+    engine.template_from_pcm(synth.load_word())
+    tm, ts = engine.get_template()
+    word = synth.load_word()
+    rng = np.random.Generator(np.random.PCG64(12))
+    good = [rng.normal(0, 1e-3, 24000).astype(np.float32) for _ in range(6)]
+    for g in good:
+        g[5000:5000 + len(word)] += word
+    bad = []
+    for k, val in enumerate((np.nan, np.inf, -np.inf)):
+        x = rng.normal(0, 1e-3, 20000 + 3000 * k).astype(np.float32)
+        x[[100, 7000, 15000]] = val
+        bad.append(x)
+    segs = [good[0], bad[0], good[1], good[2], bad[1], good[3], bad[2], good[4], good[5]]
+    _, _, score, match = engine.score(segs, candidate_dtype="float64")
+    for i, x in enumerate(segs):
+        if not np.all(np.isfinite(x)):
+            assert math.isnan(score[i]) and not match[i], (i, score[i])
+            continue
+        cm, cs = mfcc_ref.extract_mfcc(x.astype(np.float64))
+        ref = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
+        assert score_close(score[i], ref, SCORE_TOL), (i, score[i], ref)
