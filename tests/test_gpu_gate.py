@@ -239,3 +239,30 @@ def test_long_segments_cooperative_scorer(template):
             assert score_close(g[5], s, 1e-4), (i, g[1], g[5], s)
             n_long += e.length > 7 * sr
     assert n_long == 2
+
+
+def test_corrupt_stream_does_not_disturb_the_others(template):
+    """NaN / Inf samples in one stream (a broken capture) must not change any other
+    stream's events: streams are independent in the gate, the scorer and the queue."""
+    gate = dict(pre_speech_silence=0.8, speech_duration_min=0.3, speech_duration_max=2.0, post_speech_silence=0.4)
+    parts = [synth.make_stream(seed, n_words=4)[0] for seed in (61, 62, 63)]
+    L = min(len(p) for p in parts) // 1600 * 1600
+    data = np.stack([p[:L] for p in parts]).astype(np.float32)
+    bad = data.copy()
+    bad[1, 20 * 16000:20 * 16000 + 4800] = np.nan
+    bad[1, 30 * 16000:30 * 16000 + 100] = np.inf
+    got = {}
+    for name, d in (("clean", data), ("bad", bad)):
+        eng = _engine(3, gate)
+        eng.set_template(*template)
+        ev = []
+        for c in range(0, L, 8 * 1600):
+            eng.push_many(d[:, c:c + 8 * 1600])
+            ev.extend(eng.poll().tolist())
+        eng.close()
+        got[name] = ev
+    for s in (0, 2):
+        a = np.array([x[1:3] + x[5:8] for x in got["clean"] if x[0] == s], dtype=np.float64)
+        b = np.array([x[1:3] + x[5:8] for x in got["bad"] if x[0] == s], dtype=np.float64)
+        assert len(a) > 0
+        np.testing.assert_array_equal(a, b)   # (length, tick, score, match, flags); NaN == NaN
