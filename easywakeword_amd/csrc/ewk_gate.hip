@@ -710,7 +710,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
             }
             continue;
         }
-        if (lane == 0) {
+        {   // wave-uniform FSM (every lane holds the same state): no divergent branch, no broadcast
             switch (st.state) {
             case kWaiting:
                 if (silent) { st.state = kInSilence; st.silence_start = now; }
@@ -756,20 +756,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
                         ev.score = __builtin_nan("");
                         ev.match = 0;
                         ev.flags = ((double)stop / (double)g.sample_rate > g.max_segment_seconds) ? EWK_EV_SKIPPED : 0;
-                        const uint32_t slot = (uint32_t)atomicAdd(g.ev_count, 1) - (uint32_t)g.ev_base0;
-                        if (slot < (uint32_t)g.ev_cap) g.events[slot] = ev;
-                        else atomicAdd(g.ev_dropped, 1);
+                        if (lane == 0) {
+                            const uint32_t slot = (uint32_t)atomicAdd(g.ev_count, 1) - (uint32_t)g.ev_base0;
+                            if (slot < (uint32_t)g.ev_cap) g.events[slot] = ev;
+                            else atomicAdd(g.ev_dropped, 1);
+                        }
                         st.state = kWaiting;
                     }
                 } else st.state = kWaiting;
                 break;
             }
         }
-        // lane 0 owns the FSM fields; keep the wave's copy coherent
-        st.state = __shfl(st.state, 0, 64);
-        st.silence_start = __shfl(st.silence_start, 0, 64);
-        st.sound_start = __shfl(st.sound_start, 0, 64);
-        st.sound_end = __shfl(st.sound_end, 0, 64);
     }
     if (RB > 0 && (st.filled || g.compact)) {   // only the elements this launch changed (one block RMS per tick)
 #pragma unroll
