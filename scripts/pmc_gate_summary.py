@@ -16,8 +16,8 @@ def main():
     d = sys.argv[1]
     n_streams = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
     print(f"streaming-kernel PMC summary ({d}), {n_streams} streams, one tick per launch")
-    # the gate grid is capped at 1024 workgroups of 4 waves (EWK_GATE_GRID_MAX); more streams loop in-wave
-    for kern, grid in (("k_gate_ticks", min(n_streams, 4096) * 64), ("k_score_f32<", None)):
+    # the gate grid: one wave per stream up to 131,072 workgroups of 4 waves (kGateGridMax)
+    for kern, grid in (("k_gate_ticks", min(n_streams, 4 * 131072) * 64), ("k_score_f32<", None)):
         agg = collections.defaultdict(list)
         durs = []
         for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
