@@ -1544,6 +1544,9 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
         // later ones from the work counter (a burst tick's segments balance over the grid)
         for (int idx = blockIdx.x; idx < count;) {
             __syncthreads();   // wave 0's scratch (misc0) and wg_idx are free again
+            // the next index is reserved now, its atomic's latency hidden under this segment
+            int nxt = 0;
+            if (threadIdx.x == 0) nxt = (int)gridDim.x + atomicAdd(a.work, 1);
             const int seg = base + idx;
             const ewk_event ev = idx == (int)blockIdx.x ? r_ev : a.events[seg];
             if (!(ev.flags & EWK_EV_SKIPPED)) {
@@ -1555,7 +1558,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
                     score_epilogue<RING>(a, act ? misc0[lane] : 0.0f, act ? misc0[20 + lane] : 0.0f, tmf, tsf, lane,
                                          seg, v.len, listed);
             }
-            if (threadIdx.x == 0) wg_idx[0] = (int)gridDim.x + atomicAdd(a.work, 1);
+            if (threadIdx.x == 0) wg_idx[0] = nxt;
             __syncthreads();
             idx = wg_idx[0];
         }
