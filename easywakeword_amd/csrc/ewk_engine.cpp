@@ -811,10 +811,6 @@ static int push_impl(ewk_engine* e, const void* pcm_any, int64_t stride, int64_t
         g.ring_len = e->ring_len;
         g.sring_len = e->sring_len;
         g.compact = e->sring_len < e->ring_len ? 1 : 0;
-        {   // streams tick together from reset: the first tick's write position is shared
-            const int64_t bp = (e->tick * (int64_t)e->cfg.block) % e->ring_len / e->cfg.block;
-            g.blk_pred = bp < e->n_blocks ? (int32_t)bp : -1;
-        }
         g.block_rms = e->d_brms;
         g.sorted_rms = e->d_sorted;
         g.trees = e->d_trees;

@@ -69,9 +69,7 @@ struct GateArgs {
     int64_t ring_len;        // the reference ring (buffer_seconds * sample_rate): blocks, pointer, fill
     int64_t sring_len;       // samples stored per stream (== ring_len, or a compact ring: see ewk_config.ring_samples)
     int32_t compact;         // sring_len < ring_len (block-aligned; block RMSs kept from the first write)
-    int32_t blk_pred;        // the block the launch's first tick refreshes when every stream is in step
-                             // (streams tick together from reset): its old RMS is requested with the
-                             // state; -1 = none (a stream off the prediction reads its own)
+    int32_t pad0;
     double* block_rms;       // [n_streams][n_blocks] RMS of each physical block
     double* sorted_rms;      // [n_streams][2][n_blocks] the same values, ascending (double-buffered)
     GateStream* st;

@@ -282,6 +282,13 @@ __device__ __forceinline__ double reg_get(const double (&v)[RB], int i) {
     return r;
 }
 
+template <int RB>
+__device__ __forceinline__ void reg_set(double (&v)[RB], int i, double x, int lane, uint32_t& dirty) {
+#pragma unroll
+    for (int j = 0; j < RB; ++j)
+        if ((i >> 6) == j && lane == (i & 63)) { v[j] = x; dirty |= 1u << j; }
+}
+
 // so (sorted, nb values) with one occurrence of vo replaced by vn, kept sorted: the
 // new element d comes from old element d - 1, d or d + 1 (or is vn), so the update is
 // two neighbour shuffles.  Returns false when vo is absent (caller re-sorts).
@@ -455,31 +462,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
     const PwTree* tlf = trees + kTreeLastFull;
     const PwTree* tlr = trees + kTreeLastRem;
     constexpr int RBn = RB > 0 ? RB : 1;
-    // register path: the sorted multiset lives in registers (bit RB + j of `dirty`: srt[j]
-    // changed, stored back only then); the per-block array stays in memory -- a tick reads
-    // the one value it replaces (predicted block: requested with the state) and writes one
-    double srt[RBn];
-    uint32_t dirty = 0;
-    double vo_pred = 0.0;
+    double gr[RBn], srt[RBn];
+    uint32_t dirty = 0;   // register path: bit j = gr[j] changed, bit RB + j = srt[j] changed (stored back only then)
     if (RB > 0) {   // (this path never double-buffers: sorted_sel stays 0)
 #pragma unroll
         for (int j = 0; j < RBn; ++j) {
             const int i = lane + 64 * j;
+            gr[j] = i < nb ? grms[i] : 0.0;
             srt[j] = i < nb ? sorted2[i] : 0.0;
         }
-        if (g.blk_pred >= 0) vo_pred = grms[g.blk_pred];
     }
-    // the register path's rank sort (first fill / repair) from the per-block array in memory
-    // (callers fence lane 0's stores first)
-    auto rank_sort_regs = [&]() {
-        double gr[RBn];
-#pragma unroll
-        for (int j = 0; j < RBn; ++j) {
-            const int i = lane + 64 * j;
-            gr[j] = i < nb ? grms[i] : 0.0;
-        }
-        reg_rank_sort(gr, srt, nb, val, lane, dirty);
-    };
 
     for (int t = 0; t < g.n_ticks; ++t) {
         const int64_t tick = g.tick0 + t + 1;                    // tick being delivered
@@ -612,21 +604,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
                 // are whole ticks); the last one is this tick's, then the first sort
                 const int b = p0 / fs;
                 const double v = sqrt(block_sum(b) / (double)fs);
-                if (lane == 0) grms[b] = v;
+                if (RB > 0) reg_set(gr, b, v, lane, dirty);
+                else if (lane == 0) grms[b] = v;
                 __threadfence_block();
                 wave_sync();
-                if (RB > 0) rank_sort_regs();
+                if (RB > 0) reg_rank_sort(gr, srt, nb, val, lane, dirty);
                 else rank_sort(grms, sorted2, nb, lane);
                 st.sorted_sel = 0;
                 st.filled = 1;
             } else if (!st.filled) {
                 for (int b = 0; b < nb; ++b) {
                     const double sum = block_sum(b);
-                    if (lane == 0) grms[b] = sqrt(sum / (double)fs);
+                    if (RB > 0) reg_set(gr, b, sqrt(sum / (double)fs), lane, dirty);
+                    else if (lane == 0) grms[b] = sqrt(sum / (double)fs);
                 }
                 __threadfence_block();
                 wave_sync();
-                if (RB > 0) rank_sort_regs();
+                if (RB > 0) reg_rank_sort(gr, srt, nb, val, lane, dirty);
                 else rank_sort(grms, sorted2, nb, lane);
                 st.sorted_sel = 0;
                 st.filled = 1;
@@ -643,13 +637,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
                             have_reuse = true;
                         }
                         if (RB > 0) {
-                            const double vo = (t == 0 && b == g.blk_pred) ? vo_pred : grms[b];
-                            if (lane == 0) grms[b] = v;
-                            if (!reg_replace(srt, nb, vo, v, lane, dirty)) {
-                                __threadfence_block();
-                                wave_sync();
-                                rank_sort_regs();
-                            }
+                            const double vo = reg_get(gr, b);
+                            reg_set(gr, b, v, lane, dirty);
+                            if (!reg_replace(srt, nb, vo, v, lane, dirty)) reg_rank_sort(gr, srt, nb, val, lane, dirty);
                             continue;
                         }
                         const double vo = grms[b];
@@ -688,7 +678,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
             const int b = p0 / fs;
             const double v = sqrt(pw_sumsq([&](int c0) { return LdsSrc{stage + c0}; }, fs, tbf, tbr, lane, val) /
                                   (double)fs);
-            if (lane == 0) grms[b] = v;
+            if (RB > 0) reg_set(gr, b, v, lane, dirty);
+            else if (lane == 0) grms[b] = v;
         }
         // ---- a3: is_silent(): RMS of the last n_last samples < threshold
         bool silent = true;
@@ -790,10 +781,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
             }
         }
     }
-    if (RB > 0 && (st.filled || g.compact)) {   // only the sorted elements this launch moved
+    if (RB > 0 && (st.filled || g.compact)) {   // only the elements this launch changed (one block RMS per tick)
 #pragma unroll
         for (int j = 0; j < RBn; ++j) {
             const int i = lane + 64 * j;
+            if (i < nb && (dirty & (1u << j))) grms[i] = gr[j];
             if (i < nb && (dirty & (1u << (RB + j)))) sorted2[i] = srt[j];
         }
     }
