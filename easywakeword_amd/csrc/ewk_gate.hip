@@ -155,16 +155,7 @@ __device__ double tree_sumsq(const Src& src, const PwTree* t, int lane, double* 
             double r;
             { const double x = src(s0 + j); r = x * x; }
             const int lim = n - (n % 8);
-            int i = 8;
-            for (; i + 24 < lim; i += 32) {   // four reads in flight per trip, added in order
-                const double x0 = src(s0 + i + j), x1 = src(s0 + i + 8 + j);
-                const double x2 = src(s0 + i + 16 + j), x3 = src(s0 + i + 24 + j);
-                r += x0 * x0;
-                r += x1 * x1;
-                r += x2 * x2;
-                r += x3 * x3;
-            }
-            for (; i < lim; i += 8) { const double x = src(s0 + i + j); r += x * x; }
+            for (int i = 8; i < lim; i += 8) { const double x = src(s0 + i + j); r += x * x; }
             acc8[q] = r;
         }
     }
