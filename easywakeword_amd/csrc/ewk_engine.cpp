@@ -53,6 +53,7 @@ struct DevBuf {
 };
 
 constexpr int32_t kPollChunk = 1024;   // events copied speculatively with the counters
+constexpr size_t kPollRegion = 16 + (size_t)kPollChunk * sizeof(ewk_event);   // per bank: counters + chunk
 
 // Scoped temporary device buffer (freed on return; callers synchronize before).
 template <typename T>
@@ -136,6 +137,10 @@ struct ewk_engine {
     DevBuf<float> push_stage;
     float* h_stage = nullptr;       // pinned host staging for ewk_push / ewk_push_many
     unsigned char* h_poll = nullptr;   // pinned: event counters + the first kPollChunk events
+    unsigned char* d_poll = nullptr;   // h_poll's device address (k_bank_mirror writes it)
+    // mirror[b]: h_poll's region b holds bank b as of bank_done[b], written by k_bank_mirror
+    // after the push's last scoring pass (same stream) -- the poll needs no copies
+    bool mirror[2] = {false, false};
     size_t h_stage_cap = 0;
     hipEvent_t h_stage_free = nullptr;   // recorded after the last DMA out of h_stage
     int64_t tick = 0;
@@ -183,6 +188,14 @@ static void zero_event_state(ewk_engine* e) {
     e->ev_base0[0] = e->ev_base0[1] = 0;
     e->drop_base0[0] = e->drop_base0[1] = 0;
     e->bank_used[0] = e->bank_used[1] = false;
+    e->mirror[0] = e->mirror[1] = false;
+}
+
+static hipError_t ensure_poll_region(ewk_engine* e) {
+    if (e->h_poll) return hipSuccess;
+    hipError_t err = hipHostMalloc((void**)&e->h_poll, 2 * kPollRegion, hipHostMallocDefault);
+    if (err != hipSuccess) return err;
+    return hipHostGetDevicePointer((void**)&e->d_poll, e->h_poll, 0);
 }
 
 // Order stream s after every ring-mode scoring pass enqueued so far (they run on
@@ -860,6 +873,14 @@ static int push_impl(ewk_engine* e, const void* pcm_any, int64_t stride, int64_t
         }
         e->push_seq += 1;
     }
+    // the poll mirror of this bank (the overlap mode's scoring runs on sstream: copied at poll time)
+    e->mirror[e->bank] = false;
+    if (!e->overlap) {
+        HIP_TRY(ensure_poll_region(e));
+        HIP_TRY(launch_bank_mirror(e->evc_bank(e->bank), e->ev_bank(e->bank), e->ev_base0[e->bank], e->ev_cap,
+                                   std::min<int32_t>(kPollChunk, e->ev_cap), e->d_poll + e->bank * kPollRegion, s));
+        e->mirror[e->bank] = true;
+    }
     HIP_TRY(hipEventRecord(e->bank_done[e->bank], e->overlap ? e->sstream : s));
     e->bank_used[e->bank] = true;
     return EWK_OK;
@@ -995,8 +1016,6 @@ int ewk_decode_pcm16(ewk_engine* e, const int16_t* in, int64_t n, float* out, in
 // peek_bank waits for the pushes into bank b (copy stream only, no wait on later
 // work) and fetches its counters with the first kPollChunk events; take_bank copies
 // the rest out and re-arms the bank's counters on the engine stream.
-constexpr size_t kPollRegion = 16 + (size_t)kPollChunk * sizeof(ewk_event);
-
 struct BankPeek {
     int32_t n = 0;         // queued events (<= ev_cap)
     int32_t dropped = 0;   // events lost to a full bank
@@ -1007,15 +1026,19 @@ struct BankPeek {
 static int peek_bank(ewk_engine* e, int b, BankPeek* pk) {
     *pk = BankPeek();
     if (!e->bank_used[b]) return EWK_OK;
-    if (!e->h_poll) HIP_TRY(hipHostMalloc((void**)&e->h_poll, 2 * kPollRegion, hipHostMallocDefault));
+    HIP_TRY(ensure_poll_region(e));
     unsigned char* reg = e->h_poll + b * kPollRegion;
     int32_t* cnt = reinterpret_cast<int32_t*>(reg);
     const int32_t chunk = std::min<int32_t>(kPollChunk, e->ev_cap);
-    HIP_TRY(hipStreamWaitEvent(e->cstream, e->bank_done[b], 0));
-    HIP_TRY(hipMemcpyAsync(cnt, e->evc_bank(b), 4 * sizeof(int32_t), hipMemcpyDeviceToHost, e->cstream));
-    HIP_TRY(hipMemcpyAsync(reg + 16, e->ev_bank(b), (size_t)chunk * sizeof(ewk_event), hipMemcpyDeviceToHost,
-                           e->cstream));
-    HIP_TRY(hipStreamSynchronize(e->cstream));
+    if (e->mirror[b]) {   // written by k_bank_mirror behind the bank's last push
+        HIP_TRY(hipEventSynchronize(e->bank_done[b]));
+    } else {
+        HIP_TRY(hipStreamWaitEvent(e->cstream, e->bank_done[b], 0));
+        HIP_TRY(hipMemcpyAsync(cnt, e->evc_bank(b), 4 * sizeof(int32_t), hipMemcpyDeviceToHost, e->cstream));
+        HIP_TRY(hipMemcpyAsync(reg + 16, e->ev_bank(b), (size_t)chunk * sizeof(ewk_event), hipMemcpyDeviceToHost,
+                               e->cstream));
+        HIP_TRY(hipStreamSynchronize(e->cstream));
+    }
     pk->count = (uint32_t)cnt[0];
     pk->dropped_total = (uint32_t)cnt[1];
     pk->n = (int32_t)std::min<uint32_t>(pk->count - e->ev_base0[b], (uint32_t)e->ev_cap);
@@ -1030,6 +1053,7 @@ static int rearm_bank(ewk_engine* e, int b, const BankPeek& pk) {
     e->ev_base0[b] = pk.count;
     e->drop_base0[b] = pk.dropped_total;
     e->bank_used[b] = false;
+    e->mirror[b] = false;
     return EWK_OK;
 }
 

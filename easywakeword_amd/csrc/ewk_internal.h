@@ -103,6 +103,9 @@ constexpr int kRingWaveStreams = 65536;
 // ScoreArgs::order holds n_seg indices followed by kLptScratch ints of bucket counters
 constexpr int kLptScratch = 128;
 hipError_t launch_snapshot(const int32_t* src, int32_t* dst, hipStream_t s);   // *dst = *src, stream-ordered
+// counters + first min(queued, chunk) events of an event bank -> pinned host memory (poll mirror)
+hipError_t launch_bank_mirror(const int32_t* evc, const ewk_event* ev, uint32_t base0, int32_t cap, int32_t chunk,
+                              unsigned char* host, hipStream_t s);
 
 constexpr int kScoreGridMax = 256;   // one resident workgroup wave of the grid
 constexpr int kScoreGridRing = 256;                     // ring-mode grid (device-side event count)

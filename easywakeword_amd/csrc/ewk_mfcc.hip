@@ -1613,6 +1613,30 @@ hipError_t launch_snapshot(const int32_t* src, int32_t* dst, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Poll mirror of an event bank: its four counters and its first min(queued, chunk) events,
+// written straight into pinned host memory after the push's last scoring pass (stream-
+// ordered, so every score is final).  The host polls it after one event wait instead of
+// two D2H copies on a second stream (blit kernels that queue for CU slots behind the next
+// gate) and a stream synchronisation.  host: [16 B counters][chunk events], 16-B aligned.
+__global__ __launch_bounds__(256) void k_bank_mirror(const int32_t* __restrict__ evc, const ewk_event* __restrict__ ev,
+                                                     uint32_t base0, int32_t cap, int32_t chunk,
+                                                     unsigned char* __restrict__ host) {
+    const uint4 c = *reinterpret_cast<const uint4*>(evc);
+    const int32_t n = (int32_t)min(min((uint32_t)(c.x - base0), (uint32_t)cap), (uint32_t)chunk);
+    if (threadIdx.x == 0) *reinterpret_cast<uint4*>(host) = c;
+    static_assert(sizeof(ewk_event) % 16 == 0, "events copied in 16-B pieces");
+    const uint4* src = reinterpret_cast<const uint4*>(ev);
+    uint4* dst = reinterpret_cast<uint4*>(host + 16);
+    const int nq = n * (int)(sizeof(ewk_event) / 16);
+    for (int i = threadIdx.x; i < nq; i += blockDim.x) dst[i] = src[i];
+}
+
+hipError_t launch_bank_mirror(const int32_t* evc, const ewk_event* ev, uint32_t base0, int32_t cap, int32_t chunk,
+                              unsigned char* host, hipStream_t s) {
+    hipLaunchKernelGGL(k_bank_mirror, dim3(1), dim3(256), 0, s, evc, ev, base0, cap, chunk, host);
+    return hipGetLastError();
+}
+
 // Longest-first work order for a linear batch (LPT: the persistent waves' last
 // segments are the shortest, so the grid drains evenly): 64 buckets of the segment's pass
 // count, longest first; the order within a bucket is arbitrary (each segment's result
