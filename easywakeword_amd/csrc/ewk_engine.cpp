@@ -873,12 +873,12 @@ static int push_impl(ewk_engine* e, const void* pcm_any, int64_t stride, int64_t
         }
         e->push_seq += 1;
     }
-    // the poll mirror of this bank (the overlap mode's scoring runs on sstream: copied at poll time)
-    e->mirror[e->bank] = false;
-    if (!e->overlap) {
+    // the poll mirror of this bank, behind its last scoring pass (on sstream in overlap mode)
+    {
+        hipStream_t ms = e->overlap ? e->sstream : s;
         HIP_TRY(ensure_poll_region(e));
         HIP_TRY(launch_bank_mirror(e->evc_bank(e->bank), e->ev_bank(e->bank), e->ev_base0[e->bank], e->ev_cap,
-                                   std::min<int32_t>(kPollChunk, e->ev_cap), e->d_poll + e->bank * kPollRegion, s));
+                                   std::min<int32_t>(kPollChunk, e->ev_cap), e->d_poll + e->bank * kPollRegion, ms));
         e->mirror[e->bank] = true;
     }
     HIP_TRY(hipEventRecord(e->bank_done[e->bank], e->overlap ? e->sstream : s));
