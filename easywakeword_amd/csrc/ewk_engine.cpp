@@ -760,6 +760,10 @@ static int score_pending(ewk_engine* e, hipStream_t ss, const int32_t* n_events)
     a.tab64 = e->d_tab64;
     a.f64_scratch = e->f64_scratch.p;
     a.f64_per_seg = (1 + e->sring_len / HOP) * (NMEL + NMFCC);
+    HIP_TRY(ensure_poll_region(e));
+    a.mirror = e->d_poll + e->bank * kPollRegion;
+    a.evc = e->evc_bank(e->bank);
+    a.mirror_chunk = std::min<int32_t>(kPollChunk, e->ev_cap);
     {
         ProfScope ps(e, 0, ss);
         HIP_TRY(launch_score_f32(e->d_tab, a, e->n_streams >= kRingWaveStreams ? 2 : 1, ss));
@@ -873,14 +877,15 @@ static int push_impl(ewk_engine* e, const void* pcm_any, int64_t stride, int64_t
         }
         e->push_seq += 1;
     }
-    // the poll mirror of this bank, behind its last scoring pass (on sstream in overlap mode)
-    {
+    // the poll mirror of this bank: written by the last scoring pass's tick end, or (no template
+    // yet: no scoring pass) by k_bank_mirror behind the gate
+    if (!e->has_tmpl) {
         hipStream_t ms = e->overlap ? e->sstream : s;
         HIP_TRY(ensure_poll_region(e));
         HIP_TRY(launch_bank_mirror(e->evc_bank(e->bank), e->ev_bank(e->bank), e->ev_base0[e->bank], e->ev_cap,
                                    std::min<int32_t>(kPollChunk, e->ev_cap), e->d_poll + e->bank * kPollRegion, ms));
-        e->mirror[e->bank] = true;
     }
+    e->mirror[e->bank] = true;
     HIP_TRY(hipEventRecord(e->bank_done[e->bank], e->overlap ? e->sstream : s));
     e->bank_used[e->bank] = true;
     return EWK_OK;

@@ -99,6 +99,15 @@ __device__ __forceinline__ void wave_sync() {
     asm volatile("" ::: "memory");
 }
 
+// Ring samples are written once per tick and read back only for the few cut segments:
+// non-temporal stores keep them from filling the L2 with dirty lines that every launch
+// end must write back before the scorer can start.
+typedef float f32x4_nt __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void nt_store4(float* p, float4 v) {
+    f32x4_nt x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<f32x4_nt*>(p));
+}
+
 struct LdsSrc {
     const float* p;
     __device__ __forceinline__ float operator()(int i) const { return p[i]; }
@@ -497,7 +506,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
                     if (i < fs) {
                         int k = sp0 + i;
                         if (k >= Rs) k -= Rs;
-                        *reinterpret_cast<float4*>(ring + k) = xv[c];
+                        nt_store4(ring + k, xv[c]);
                     }
                 }
                 if (256 * (h + 4) >= fs) break;
@@ -537,10 +546,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
                         v[2 * h + 1] = (float)((int)w[h] >> 16) * (1.0f / 32768.0f);
                     }
                     if (ring16) {
-                        *reinterpret_cast<u32x4*>(ring16 + k) = w;
+                        __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(ring16 + k));
                     } else {
-                        *reinterpret_cast<float4*>(ring + k) = make_float4(v[0], v[1], v[2], v[3]);
-                        *reinterpret_cast<float4*>(ring + k + 4) = make_float4(v[4], v[5], v[6], v[7]);
+                        nt_store4(ring + k, make_float4(v[0], v[1], v[2], v[3]));
+                        nt_store4(ring + k + 4, make_float4(v[4], v[5], v[6], v[7]));
                     }
                     if (staged) {
                         *reinterpret_cast<float4*>(stage + i0) = make_float4(v[0], v[1], v[2], v[3]);

@@ -93,6 +93,11 @@ struct ScoreArgs {
     const struct Tables64* tab64;   // fp64 re-score tables
     double* f64_scratch;      // fp64 re-score: [slot][f64_per_seg] log-mel + mfcc rows
     int64_t f64_per_seg;
+    // ring mode poll mirror (nullptr: none): the last workgroup copies the bank's counters
+    // (evc) and its first min(queued, mirror_chunk) events into pinned host memory
+    unsigned char* mirror;
+    const int32_t* evc;
+    int32_t mirror_chunk;
 };
 
 // ring_mode: 0 linear batch, 1 ring events one segment per workgroup, 2 ring events one

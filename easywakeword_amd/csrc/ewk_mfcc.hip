@@ -1345,6 +1345,7 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, fl
         if (RING) {
             a.events[seg].score = score;
             a.events[seg].match = match;
+            if (a.mirror) listed = true;   // the last workgroup copies this event to the poll mirror
         } else {
             a.out_score[seg] = score;
             if (a.out_match) a.out_match[seg] = (uint8_t)match;
@@ -1424,6 +1425,20 @@ __device__ void ring_tick_end(const ScoreArgs& a, unsigned char* smem, bool list
         *a.rescore_count = 0;
         *a.adv_done = 0;
         __threadfence();
+    }
+    if (a.mirror) {   // poll mirror: the bank's counters and first events -> pinned host memory
+        __syncthreads();   // this workgroup's re-score writes are done and fenced by thread 0
+        const volatile int32_t* vc = a.evc;
+        const uint4 c = make_uint4((uint32_t)vc[0], (uint32_t)vc[1], (uint32_t)vc[2], (uint32_t)vc[3]);
+        const int32_t n = (int32_t)min(min((uint32_t)(c.x - (uint32_t)a.ev_base0), (uint32_t)a.n_seg),
+                                       (uint32_t)a.mirror_chunk);
+        if (threadIdx.x == 0) *reinterpret_cast<uint4*>(a.mirror) = c;
+        const uint4* src = reinterpret_cast<const uint4*>(a.events);
+        uint4* dst = reinterpret_cast<uint4*>(a.mirror + 16);
+        const int nq = n * (int)(sizeof(ewk_event) / 16);
+        // every workgroup that wrote a score released it before its arrival count, and thread
+        // 0's device-scope fence above (after the last arrival) acquired them for this workgroup
+        for (int i = threadIdx.x; i < nq; i += blockDim.x) dst[i] = src[i];
     }
 }
 static_assert(WAVES * 256 * 16 + WAVES * (NBIN + 3) * 8 + NFFT * 8 + 128 * 16 + NBIN * 16 + NMFCC * NMEL * 8 +

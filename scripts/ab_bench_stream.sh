@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=${1:-2}; BIG=${2:-0}; MAX=${3:-0}
 for r in $(seq 1 $R); do
-  for f in variants/*.so; do
+  for f in ${VDIR:-variants}/*.so; do
     echo -n "$(basename $f) "
     EWK_LIB=$PWD/$f timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --fixed-len 0 --confirm-batch 0 \
         --big-streams $BIG --max-streams $MAX 2>/dev/null | \

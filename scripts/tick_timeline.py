@@ -8,7 +8,7 @@ f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
 rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
 rows = [r for r in rows if "ewk::" in r["Kernel_Name"] or "rocclr" in r["Kernel_Name"]]
 def short(n):
-    for k in ("k_gate_ticks", "k_score_f32<1, 0>", "k_score_f64<1>", "k_advance", "copyBuffer", "fillBuffer", "k_snapshot", "k_normalize"):
+    for k in ("k_gate_ticks", "k_score_f32<1, 0>", "k_score_f64<1>", "k_advance", "copyBuffer", "fillBuffer", "k_snapshot", "k_normalize", "k_bank_mirror"):
         if k in n:
             return k
     return n[:30]
