@@ -99,3 +99,50 @@ def test_random_stream_configs_vs_oracle(seed, template):
             assert bool(m["match"]) == (s >= 75.0), (c, i)
             n_scored += 1
     assert n_scored >= 1, c
+
+
+@pytest.mark.parametrize("overlap", ["0", "1"])
+def test_lagged_polls_late_template_and_overlap_vs_oracle(overlap, template, monkeypatch):
+    """One tick per push with lagged polls (the serving cadence), the template set only after
+    tick 150 (the polls before it read the k_bank_mirror copy, after it the scorer's tick-end
+    copy), with the scorer on the engine stream and in the opt-in overlap mode
+    (EWK_SCORE_OVERLAP=1, scoring of tick t beside the gate of tick t+1): the event list equals
+    the oracle's, every scored event within 1e-4 of it, every event after the template scored."""
+    from easywakeword_amd import StreamEngine
+    monkeypatch.setenv("EWK_SCORE_OVERLAP", overlap)
+    block, n = 1600, 4
+    pcms = [synth.make_stream(seed=7100 + i, n_words=4, prefill=10.5, sigma=1e-3, gain=1.0,
+                              distractors=bool(i % 2), block=block)[0] for i in range(n)]
+    L = min(len(p) for p in pcms)
+    L -= L % block
+    data = np.stack([p[:L] for p in pcms]).astype(np.float32)
+    eng = StreamEngine(n, block=block, tick_seconds=block / SR, buffer_seconds=10)
+    t_tmpl = 150
+    got = []
+    for t in range(L // block):
+        if t == t_tmpl:
+            eng.set_template(*template)
+        eng.push_many(data[:, t * block:(t + 1) * block])
+        got.append(eng.poll(lagged=True))
+    got.append(eng.poll())
+    eng.close()
+    ev = np.concatenate(got)
+    tm, ts = template
+    gcfg = GateConfig(block=block, tick_seconds=block / SR, buffer_seconds=10)
+    n_scored = 0
+    for i in range(n):
+        ref = run_stream(data[i], gcfg).events
+        mine = ev[ev["stream"] == i]
+        assert [(int(m["tick"]), int(m["length"]), bool(m["flags"] & 1)) for m in mine] == \
+               [(e.tick, e.length, e.skipped) for e in ref], (overlap, i)
+        for m, e in zip(mine, ref):
+            if e.skipped:
+                continue
+            if np.isnan(float(m["score"])) and int(m["tick"]) <= t_tmpl:
+                continue   # drained before the template existed: never scored
+            cm, cs = mfcc_ref.extract_mfcc(e.audio)
+            s = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
+            assert score_close(float(m["score"]), s, 1e-4), (overlap, i, int(m["tick"]), float(m["score"]), s)
+            assert bool(m["match"]) == (s >= 75.0), (overlap, i)
+            n_scored += 1
+    assert n_scored >= 1
