@@ -1,9 +1,10 @@
 """Per-tick GPU timeline of the streaming loop from a rocprofv3 --kernel-trace csv:
 kernel durations and the idle gaps between consecutive dispatches (all queues).
-Usage: python scripts/tick_timeline.py <dir with *_kernel_trace.csv> [ticks shown]"""
+Usage: python scripts/tick_timeline.py <dir with *_kernel_trace.csv> [ticks shown] [last tick index, default -1]"""
 import csv, glob, os, sys
 d = sys.argv[1]
 show = int(sys.argv[2]) if len(sys.argv) > 2 else 6
+end = int(sys.argv[3]) if len(sys.argv) > 3 else -1   # e.g. 420: inside the un-instrumented timed ticks
 f = glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True)[0]
 rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Start_Timestamp"]))
 rows = [r for r in rows if "ewk::" in r["Kernel_Name"] or "rocclr" in r["Kernel_Name"]]
@@ -14,7 +15,8 @@ def short(n):
     return n[:30]
 gates = [i for i, r in enumerate(rows) if "k_gate_ticks" in r["Kernel_Name"]]
 per_tick = []
-for a, b in zip(gates[-show - 1:-1], gates[-show:]):
+sel = gates[:end + 1] if end >= 0 else gates
+for a, b in zip(sel[-show - 1:-1], sel[-show:]):
     t0 = int(rows[a]["Start_Timestamp"])
     t1 = int(rows[b]["Start_Timestamp"])
     parts, prev_end = [], t0
