@@ -502,6 +502,14 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
     return out
 
 
+def _rccl_version(torch):
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception as exc:   # noqa: BLE001 - reported, not fatal
+        return f"unavailable ({type(exc).__name__})"
+
+
 # --------------------------------------------------------------------------- main
 def main():
     args = parse()
@@ -542,17 +550,27 @@ def main():
     assert sh != 0
     if world > 1:   # positives only: device compaction, counts all_gather, P2P records (tests/test_dist_gloo.py)
         from easywakeword_amd.shard import MatchGather
-        gather = MatchGather(n_seg, rank * n_seg, cdev)
+        # the matched segments' (id, score, step) records stay on the device across the
+        # steps of a loop and go to rank 0 (the confirm stage's input) in ONE gather per
+        # loop: no host sync inside the loop
+        gather = MatchGather(n_seg, rank * n_seg, cdev, steps=max(args.steps, args.warmup, 1))
+    gathered = [0]
 
     def step():
         eng.score_device(pcm.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n_seg, mean.data_ptr(),
                          std.data_ptr(), score.data_ptr(), match.data_ptr(), sh)
-        if world > 1:   # the matched segments' (id, score) records -> rank 0 (the confirm stage's input)
-            gather(score.to(cdev), match.to(cdev))
+        if world > 1:
+            gather.add(score.to(cdev), match.to(cdev))
+
+    def flush():
+        if world > 1:
+            rec = gather.flush()
+            gathered[0] = 0 if rec is None else int(rec.shape[0])
 
     torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
+    flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -564,6 +582,7 @@ def main():
     ev0.record(stream)
     for _ in range(args.steps):
         step()
+    flush()   # the K steps' positives -> rank 0, inside the timed region
     ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -651,6 +670,11 @@ def main():
     }
     if fixed is not None:
         out["fixed_length"] = fixed
+    if world > 1:   # what the collectives actually ran on (a SCALE run can check RCCL saw N ranks)
+        out["distributed"] = {"world_size_seen": dist.get_world_size(), "backend": str(dist.get_backend()),
+                              "rccl_version": _rccl_version(torch), "positives_gathered_to_rank0": gathered[0],
+                              "gather": "positives held on the device over the timed loop, one counts all_gather + "
+                                        "point-to-point records to rank 0 after its last step (inside the timing)"}
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sample = min(n_seg, max(16, host_cores()[0]) * 400)

@@ -31,6 +31,7 @@ EWK_RING_F32 = 0
 EWK_RING_I16 = 1
 EWK_SCORE_REQUIRE_TEMPLATE = 1
 EWK_SCORE_F32_CANDIDATES = 2
+EWK_COMPACT_APPEND = 1
 
 # Every symbol include/ewk.h declares (checked by tests/test_capi.py).
 EXPORTS = [
@@ -42,7 +43,7 @@ EXPORTS = [
     "ewk_read_segment", "ewk_reset_streams", "ewk_set_similarity_threshold",
     "ewk_profile_enable", "ewk_profile_read",
     "ewk_push_pcm16", "ewk_push_many_pcm16", "ewk_normalize_segments", "ewk_normalize_events",
-    "ewk_decode_pcm16", "ewk_poll_lagged", "ewk_runtime_info", "ewk_reenter",
+    "ewk_decode_pcm16", "ewk_poll_lagged", "ewk_runtime_info", "ewk_reenter", "ewk_compact_positives",
 ]
 
 
@@ -68,6 +69,14 @@ class EwkEvent(C.Structure):
 EVENT_DTYPE = np.dtype([("stream", "<i4"), ("length", "<i4"), ("tick", "<i8"), ("ring_start", "<i8"),
                         ("time", "<f8"), ("score", "<f8"), ("match", "<i4"), ("flags", "<i4")])
 assert EVENT_DTYPE.itemsize == C.sizeof(EwkEvent)
+
+
+class EwkPositive(C.Structure):
+    _fields_ = [("id", C.c_int64), ("score", C.c_double), ("step", C.c_int64)]
+
+
+POSITIVE_DTYPE = np.dtype([("id", "<i8"), ("score", "<f8"), ("step", "<i8")])
+assert POSITIVE_DTYPE.itemsize == C.sizeof(EwkPositive)
 
 
 class EwkStreamState(C.Structure):
@@ -146,6 +155,7 @@ def load():
             "ewk_normalize_segments": (C.c_int, [_P, _P, C.c_int64, _i64p, _i32p, C.c_int32, _P, C.c_int32]),
             "ewk_normalize_events": (C.c_int, [_P, C.POINTER(EwkEvent), C.c_int32, _P, C.c_int32]),
             "ewk_decode_pcm16": (C.c_int, [_P, _P, C.c_int64, _P, C.c_int32]),
+            "ewk_compact_positives": (C.c_int, [_P, _P, _P, C.c_int32, C.c_int64, C.c_int64, _P, _P, C.c_int32, _P]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)

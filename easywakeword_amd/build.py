@@ -13,7 +13,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["ewk_mfcc.hip", "ewk_gate.hip", "ewk_level3.hip", "ewk_engine.cpp", "ewk_tables.cpp"]
+SOURCES = ["ewk_mfcc.hip", "ewk_gate.hip", "ewk_level3.hip", "ewk_gather.hip", "ewk_engine.cpp", "ewk_tables.cpp"]
 HEADERS = ["ewk_internal.h", "ewk_gate.h", os.path.join("..", "..", "include", "ewk.h")]
 LIB = os.path.join(HERE, "libewk.so")
 ARCH = os.environ.get("EWK_OFFLOAD_ARCH", "gfx950")

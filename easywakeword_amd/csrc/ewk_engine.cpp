@@ -84,6 +84,8 @@ struct ewk_engine {
     DevBuf<int32_t> rescore_buf;    // [0] = count, [1..] list
     int32_t* d_rescore = nullptr;   // == rescore_buf.p
     int32_t* d_work = nullptr;      // scorer work counter
+    int32_t* d_compact = nullptr;   // ewk_compact_positives block counts / offsets
+    int32_t compact_cap = 0;        // ... in blocks
     DevBuf<int32_t> order;          // linear batches: longest-first work order (k_lpt_order)
     int32_t rescore_cap = 4096;
     DevBuf<double> f64_scratch;
@@ -192,10 +194,18 @@ static void zero_event_state(ewk_engine* e) {
 }
 
 static hipError_t ensure_poll_region(ewk_engine* e) {
-    if (e->h_poll) return hipSuccess;
-    hipError_t err = hipHostMalloc((void**)&e->h_poll, 2 * kPollRegion, hipHostMallocDefault);
-    if (err != hipSuccess) return err;
-    return hipHostGetDevicePointer((void**)&e->d_poll, e->h_poll, 0);
+    if (e->h_poll && e->d_poll) return hipSuccess;
+    if (!e->h_poll) {
+        hipError_t err = hipHostMalloc((void**)&e->h_poll, 2 * kPollRegion, hipHostMallocDefault);
+        if (err != hipSuccess) { e->h_poll = nullptr; return err; }
+    }
+    hipError_t err = hipHostGetDevicePointer((void**)&e->d_poll, e->h_poll, 0);
+    if (err != hipSuccess) {   // never leave a host region without its device alias (the mirror writes through it)
+        (void)hipHostFree(e->h_poll);
+        e->h_poll = nullptr;
+        e->d_poll = nullptr;
+    }
+    return err;
 }
 
 // Order stream s after every ring-mode scoring pass enqueued so far (they run on
@@ -281,6 +291,7 @@ void ewk_destroy(ewk_engine* e) {
     (void)hipFree(e->d_tmpl);
     e->rescore_buf.release();
     (void)hipFree(e->d_work);
+    (void)hipFree(e->d_compact);
     e->f64_scratch.release();
     e->order.release();
     e->pcm.release();
@@ -987,12 +998,50 @@ int ewk_normalize_events(ewk_engine* e, const ewk_event* events, int32_t n, doub
     if (n == 0) return EWK_OK;
     if (!events || !out) return fail(EWK_EINVAL, "NULL argument");
     if (e->n_streams <= 0) return fail(EWK_EINVAL, "engine has no streams");
-    for (int32_t i = 0; i < n; ++i)
-        if (events[i].stream < 0 || events[i].stream >= e->n_streams || events[i].length < 0 ||
-            events[i].length > e->sring_len || events[i].ring_start < 0 || events[i].ring_start >= e->sring_len)
+    for (int32_t i = 0; i < n; ++i) {
+        const ewk_event& ev = events[i];
+        if (ev.stream < 0 || ev.stream >= e->n_streams || ev.length < 0 || ev.length > e->sring_len ||
+            ev.ring_start < 0 || ev.ring_start >= e->sring_len)
             return fail(EWK_EINVAL, "event " + std::to_string(i) + " outside the rings");
+        // The segment is the last nreq >= length samples before the write position of its
+        // tick (ewk_gate.hip, the cut), and every later tick writes one block: it is intact
+        // while nreq + (ticks since) * block <= ring.  (The write position after tick k is
+        // k * block mod ring for every stream.)
+        const int64_t Rs = e->sring_len, blk = e->cfg.block;
+        if (ev.tick < 0 || ev.tick > e->tick)
+            return fail(EWK_EINVAL, "event " + std::to_string(i) + " is from a tick this engine has not pushed");
+        int64_t nreq = ((ev.tick % Rs) * (blk % Rs) % Rs - ev.ring_start) % Rs;
+        if (nreq < 0) nreq += Rs;
+        if (nreq == 0 && ev.length > 0) nreq = Rs;
+        if (nreq + (e->tick - ev.tick) * blk > Rs)
+            return fail(EWK_EINVAL, "event " + std::to_string(i) + " (tick " + std::to_string(ev.tick) +
+                                        "): the ring has overwritten its samples since (now tick " +
+                                        std::to_string(e->tick) + "); read positives right after their poll");
+    }
     HIP_TRY(hipSetDevice(e->device));
     return normalize_impl(e, nullptr, nullptr, nullptr, events, n, out, flags);
+}
+
+int ewk_compact_positives(ewk_engine* e, const double* d_score, const uint8_t* d_match, int32_t n, int64_t first_id,
+                          int64_t step, ewk_positive* d_out, int32_t* d_count, int32_t flags, void* stream) {
+    if (!e) return fail(EWK_EINVAL, "engine is NULL");
+    if (n < 0) return fail(EWK_EINVAL, "negative size");
+    if (!d_count || (n > 0 && (!d_score || !d_match || !d_out))) return fail(EWK_EINVAL, "NULL argument");
+    if (flags & ~EWK_COMPACT_APPEND) return fail(EWK_EINVAL, "unknown flags");
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : e->stream;
+    const int nb = std::max(1, compact_blocks(n));
+    if (nb > e->compact_cap) {   // grown rarely (stream-ordered: the old scratch may be in use)
+        HIP_TRY(hipStreamSynchronize(s));
+        (void)hipFree(e->d_compact);
+        e->d_compact = nullptr;
+        e->compact_cap = 0;
+        HIP_TRY(hipMalloc(&e->d_compact, 2 * (size_t)nb * sizeof(int32_t)));
+        e->compact_cap = nb;
+    }
+    HIP_TRY(launch_compact_positives(d_score, d_match, n, first_id, step, d_out, d_count, e->d_compact,
+                                     (flags & EWK_COMPACT_APPEND) ? 1 : 0, s));
+    return EWK_OK;
 }
 
 int ewk_decode_pcm16(ewk_engine* e, const int16_t* in, int64_t n, float* out, int32_t flags) {

@@ -136,4 +136,10 @@ struct L3Args {
 hipError_t launch_normalize(const L3Args& a, hipStream_t s);
 hipError_t launch_decode_pcm16(const int16_t* in, float* out, int64_t n, hipStream_t s);
 
+// ewk_gather.hip: positives compaction (scratch: 2 * compact_blocks(n) int32)
+int compact_blocks(int32_t n);
+hipError_t launch_compact_positives(const double* score, const uint8_t* match, int32_t n, int64_t first_id,
+                                    int64_t step, ewk_positive* out, int32_t* d_count, int32_t* scratch, int append,
+                                    hipStream_t s);
+
 }  // namespace ewk

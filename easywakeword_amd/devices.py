@@ -33,6 +33,10 @@ def _sd(sd=None):
     return sounddevice
 
 
+class NoInputDeviceError(ValueError):
+    """No audio input device exists at all (as opposed to a spec that matches none)."""
+
+
 class AudioDeviceManager:
     """Input-device selection (wakeword.py:51-402)."""
 
@@ -101,7 +105,7 @@ class AudioDeviceManager:
         sd = _sd(sd)
         devices = AudioDeviceManager.list_devices(sd)
         if not devices:
-            raise ValueError("no audio input devices found")
+            raise NoInputDeviceError("no audio input devices found")
         if spec is None:
             idx = AudioDeviceManager._system_default(sd)
             if idx is not None:

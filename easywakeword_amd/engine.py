@@ -194,6 +194,18 @@ class Engine:
                                                   C.c_void_p(stream or None)))
 
 
+    def compact_positives_device(self, score_ptr: int, match_ptr: int, n: int, first_id: int, out_ptr: int,
+                                 count_ptr: int, step: int = 0, append: bool = False, stream: int = 0) -> None:
+        """Matched segments of a device batch -> ewk_positive records {id, score, step} at
+        out_ptr (device, segment order) and their int32 count at count_ptr (device); with
+        append=True after the count already there.  Asynchronous on `stream`, no host sync:
+        the buffers go straight to an RCCL gather (include/ewk.h, ewk_compact_positives)."""
+        check(self._lib.ewk_compact_positives(self._h, C.c_void_p(score_ptr or None), C.c_void_p(match_ptr or None),
+                                              int(n), int(first_id), int(step), C.c_void_p(out_ptr or None),
+                                              C.c_void_p(count_ptr or None),
+                                              _lib.EWK_COMPACT_APPEND if append else 0, C.c_void_p(stream or None)))
+
+
 class StreamEngine(Engine):
     """N concurrent 16 kHz streams on one GPU: ring + adaptive threshold + timing
     FSM per stream (level 1) and MFCC matching of every gated segment (level 2)."""
@@ -274,7 +286,9 @@ class StreamEngine(Engine):
         """Drain queued events as a structured array (see _lib.EVENT_DTYPE).
         lagged=True: the events of the pushes before the previous lagged poll, without
         waiting for the latest push (pipelined serving; see include/ewk.h)."""
-        cap = int(cap or max(4096, 4 * self.n_streams))
+        # a non-lagged poll drains both event banks (each holds up to the engine's queue
+        # capacity after a lagged poll), so its default buffer holds two banks
+        cap = int(cap or (1 if lagged else 2) * max(4096, 4 * self.n_streams))
         if getattr(self, "_poll_buf", None) is None or len(self._poll_buf) < cap:
             self._poll_buf = np.zeros(cap, dtype=_lib.EVENT_DTYPE)   # reused: polled every tick
             self._poll_n = C.c_int32(0)

@@ -6,9 +6,10 @@ and scores their segments on its own GPU.  The only exchange is the gather of
 POSITIVE detections to one rank -- the input of the optional level-3 confirm,
 which the reference runs once per detection (wakeword.py:1120-1130):
 
-* ``MatchGather``       (batch scorer step) device-side compaction of the matched
-                        segments' (id, score) records, no host sync before the
-                        collectives, then ``gather_positives``;
+* ``MatchGather``       (batch scorer steps) device-side compaction of the matched
+                        segments' (id, score, step) records, appended step after
+                        step with no host sync, then one ``gather_positives`` per
+                        flush (every K steps);
 * ``PositiveCollector`` (streaming) accumulates each tick's polled positives and
                         gathers them every ``every`` ticks, with the level-3 input
                         PCM of up to ``audio_cap`` of them per rank;
@@ -110,33 +111,61 @@ def gather_positives(records, audio=None, count=None, group=None, dst: int = 0):
 
 
 class MatchGather:
-    """Batch scorer step on N ranks: the matched segments' records go to `dst`.
+    """Batch scorer steps on N ranks: the matched segments' records go to `dst`.
 
-    Device-side compaction into a persistent [n_seg, 2] int64 buffer (column 0 =
-    global segment id first_id + i, column 1 = the float64 score's bits), with the
-    count left on the device: no host sync until the counts' all_gather, and only
-    positives cross xGMI (not the per-segment score/match arrays).
+    Device-side compaction into a persistent [steps * n_seg + 1, 3] int64 buffer
+    (column 0 = global segment id first_id + i, column 1 = the float64 score's bits,
+    column 2 = the step index since the last flush), with the running count left on the
+    device: ``add`` appends one step's positives without any host sync, ``flush``
+    gathers everything held so far -- one counts all_gather (the only host sync) plus
+    point-to-point records per flush, however many steps it covers -- and only
+    positives cross xGMI (never the per-segment score/match arrays).
     """
 
-    def __init__(self, n_seg: int, first_id: int, device, group=None, dst: int = 0):
+    def __init__(self, n_seg: int, first_id: int, device, steps: int = 1, group=None, dst: int = 0):
         import torch
-        self.n_seg, self.first_id, self.group, self.dst = n_seg, first_id, group, dst
-        self.buf = torch.zeros((n_seg + 1, 2), dtype=torch.int64, device=device)   # row n_seg: discard slot
+        if steps < 1:
+            raise ValueError("steps must be >= 1")
+        self.n_seg, self.first_id, self.steps, self.group, self.dst = n_seg, first_id, steps, group, dst
+        self.cap = n_seg * steps
+        self.buf = torch.zeros((self.cap + 1, 3), dtype=torch.int64, device=device)   # row cap: discard slot
         self.ids = torch.arange(first_id, first_id + n_seg, dtype=torch.int64, device=device)
+        self.count = torch.zeros(1, dtype=torch.int64, device=device)
+        self.held = 0   # steps added since the last flush (host-side: no sync needed)
+
+    def add(self, score, match) -> None:
+        """Append one step's matches (device ops only; raises once `steps` are held)."""
+        import torch
+        if self.held >= self.steps:
+            raise RuntimeError(f"MatchGather holds {self.steps} steps: flush() first")
+        m = match.reshape(-1).to(torch.int64)
+        pos = self.count + torch.cumsum(m, 0) - 1
+        tgt = torch.where(m.bool(), pos, torch.full_like(pos, self.cap))
+        vals = torch.stack([self.ids, score.reshape(-1).to(torch.float64).view(torch.int64),
+                            torch.full_like(self.ids, self.held)], 1)
+        self.buf.index_copy_(0, tgt, vals)
+        self.count += m.sum()
+        self.held += 1
 
     def compact(self, score, match):
-        """(records [n_seg + 1, 2], count [1]) with records[:count] the matches in index order."""
-        import torch
-        m = match.reshape(-1).to(torch.int64)
-        pos = torch.cumsum(m, 0) - 1
-        tgt = torch.where(m.bool(), pos, torch.full_like(pos, self.n_seg))
-        vals = torch.stack([self.ids, score.reshape(-1).to(torch.float64).view(torch.int64)], 1)
-        self.buf.index_copy_(0, tgt, vals)
-        return self.buf, pos[-1:] + 1
+        """One step on its own: (records [cap + 1, 3], count [1]), records[:count] in index order."""
+        self.count.zero_()
+        self.held = 0
+        self.add(score, match)
+        return self.buf, self.count
+
+    def flush(self):
+        """Gather every held record to `dst` (records on `dst`, None elsewhere) and re-arm."""
+        rec = gather_positives(self.buf, count=self.count, group=self.group, dst=self.dst)[0]
+        if rec is not None:
+            rec = rec.clone()   # the buffer is reused by the next add()
+        self.count.zero_()
+        self.held = 0
+        return rec
 
     def __call__(self, score, match):
-        rec, cnt = self.compact(score, match)
-        return gather_positives(rec, count=cnt, group=self.group, dst=self.dst)[0]
+        self.compact(score, match)
+        return self.flush()
 
 
 class PositiveCollector:
@@ -145,21 +174,51 @@ class PositiveCollector:
     {global stream, tick, length, score bits} plus the level-3 input PCM of the newest
     `audio_cap` of them per rank (`audio_fn(events) -> list of 1-D tensors`, e.g.
     StreamEngine.normalize_events_device: the normalised audio, wakeword.py:1019-1025,
-    straight from the rings)."""
+    straight from the rings).
+
+    The PCM is captured in ``add`` -- right after the poll that returned the events, while
+    the segments are still in the rings (a compact ring keeps only the longest request
+    plus one tick; ten ticks later the start of a long utterance is gone) -- and only the
+    newest `audio_cap` captures are kept until the flush.
+    """
 
     def __init__(self, first_stream: int, device, every: int = 10, audio_cap: int = 64,
                  audio_fn: Optional[Callable] = None, group=None, dst: int = 0):
         self.first_stream, self.device, self.every, self.audio_cap = first_stream, device, every, audio_cap
         self.audio_fn, self.group, self.dst = audio_fn, group, dst
-        self.pending = []
+        self.pending = []      # positives without captured PCM
+        self.captured = []     # [(events, pcm list)] newest first, <= audio_cap events in all
         self.ticks = 0
         self.gathered = 0
         self.gathered_audio = 0
 
+    @staticmethod
+    def _newest_first(ev: np.ndarray) -> np.ndarray:
+        return ev[np.lexsort((ev["stream"], -ev["tick"]))]
+
     def add(self, events: np.ndarray) -> None:
         pos = events[(events["match"] != 0) & ((events["flags"] & 1) == 0)]
-        if len(pos):
+        if not len(pos):
+            return
+        if self.audio_fn is None or self.audio_cap <= 0:
             self.pending.append(pos)
+            return
+        pos = self._newest_first(pos)
+        take = pos[:self.audio_cap]
+        if len(pos) > len(take):
+            self.pending.append(pos[len(take):])
+        self.captured.insert(0, (take, list(self.audio_fn(take))))   # polls arrive in tick order
+        kept = 0
+        for i, (ev, pcm) in enumerate(self.captured):   # keep the newest audio_cap captures
+            room = self.audio_cap - kept
+            if room <= 0:
+                self.pending.extend(e for e, _ in self.captured[i:])
+                del self.captured[i:]
+                break
+            if len(ev) > room:
+                self.pending.append(ev[room:])
+                self.captured[i] = (ev[:room], pcm[:room])
+            kept += len(self.captured[i][0])
 
     def tick(self, n: int = 1):
         """Count n ticks; gathers when `every` ticks have passed (returns flush()'s result)."""
@@ -171,19 +230,19 @@ class PositiveCollector:
     def flush(self):
         import torch
         self.ticks = 0
-        ev = np.concatenate(self.pending) if self.pending else None
-        self.pending = []
-        if ev is None or not len(ev):
-            rec = np.zeros((0, 4), np.int64)
-            ev = None
-        else:
-            # newest first, so the PCM rides with the first audio_cap records
-            ev = ev[np.lexsort((ev["stream"], -ev["tick"]))]
+        cap_ev = [e for e, _ in self.captured]
+        audio = [x for _, pcm in self.captured for x in pcm] if self.audio_fn is not None else None
+        rest = np.concatenate(self.pending) if self.pending else None
+        rest = self._newest_first(rest) if rest is not None and len(rest) else None
+        parts = cap_ev + ([rest] if rest is not None else [])
+        self.pending, self.captured = [], []
+        if parts:
+            # the records with captured PCM first, in the order of their PCM
+            ev = np.concatenate(parts)
             rec = np.stack([ev["stream"].astype(np.int64) + self.first_stream, ev["tick"].astype(np.int64),
                             ev["length"].astype(np.int64), ev["score"].astype(np.float64).view(np.int64)], axis=1)
-        audio = None
-        if self.audio_fn is not None:
-            audio = list(self.audio_fn(ev[:self.audio_cap])) if ev is not None and self.audio_cap > 0 else []
+        else:
+            rec = np.zeros((0, 4), np.int64)
         out_rec, out_audio = gather_positives(torch.from_numpy(rec).to(self.device), audio=audio,
                                               group=self.group, dst=self.dst)
         if out_rec is not None:

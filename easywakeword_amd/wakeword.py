@@ -183,11 +183,11 @@ def _default_source(device):
     """The microphone `device` names (None, index, name pattern, "default"/"best"/"first"),
     resolved like the reference's AudioDeviceManager.select_device (wakeword.py:128-185,
     437); an unmatched spec raises ValueError instead of falling back to the default mic."""
-    from .devices import AudioDeviceManager
+    from .devices import AudioDeviceManager, NoInputDeviceError
     try:
         index = AudioDeviceManager.select_device(device)
         return _audio.MicSource(device=index, block=BLOCK)
-    except (ImportError, OSError) as exc:
+    except (ImportError, OSError, NoInputDeviceError) as exc:   # a spec matching nothing stays ValueError
         raise OSError("no audio input available (sounddevice/PortAudio missing); "
                       "pass source=ArraySource(...) or WavSource(...)") from exc
 

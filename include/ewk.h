@@ -225,6 +225,27 @@ int ewk_normalize_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const
 /* ... or gated segments straight from the stream rings (polled events: stream,
  * ring_start, length), the reference's word_audio of each event. */
 int ewk_normalize_events(ewk_engine* e, const ewk_event* events, int32_t n, double* out, int32_t flags);
+/* Positives for the level-3 confirm gather (SURVEY.md 8b `ewk_gather_detections`, 8e):
+ * the reference confirms every detection (wakeword.py:1120-1130); on N GPUs only the
+ * positives cross xGMI.  Compacts the matched segments of a scored batch -- d_score /
+ * d_match as ewk_score_segments_device wrote them -- into d_out (device memory,
+ * capacity >= n, or >= *d_count + n with EWK_COMPACT_APPEND) in segment order, record
+ * i = {first_id + segment index, score, step}, and leaves the count in *d_count (device
+ * memory): no host sync, so a C/C++ host can hand d_out / d_count straight to its own
+ * RCCL collective.  EWK_COMPACT_APPEND keeps the *d_count
+ * records already there (K steps batched into one gather, the batch step of
+ * easywakeword_amd.shard.MatchGather); otherwise *d_count is overwritten.
+ * Asynchronous on `stream` (NULL = the engine's stream); the engine's scratch is shared,
+ * so calls on different streams must be ordered by the caller. */
+#define EWK_COMPACT_APPEND 1
+typedef struct ewk_positive {
+    int64_t id;                   /* first_id + index of the segment in its batch */
+    double score;                 /* its scaled similarity (>= threshold) */
+    int64_t step;                 /* caller's step tag (e.g. the batch number) */
+} ewk_positive;
+int ewk_compact_positives(ewk_engine* e, const double* d_score, const uint8_t* d_match, int32_t n,
+                          int64_t first_id, int64_t step, ewk_positive* d_out, int32_t* d_count,
+                          int32_t flags, void* stream);
 /* WAV / PCM16 ingest (librosa.load of a 16 kHz PCM16 file = int16 / 32768 as float32):
  * host arrays unless EWK_PCM_DEVICE (then both are device memory, asynchronous). */
 int ewk_decode_pcm16(ewk_engine* e, const int16_t* in, int64_t n, float* out, int32_t flags);

@@ -11,7 +11,8 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 16384
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
 dev = torch.device("cuda", 0)
 word = bench.load_word()
-pcm, off, ln, frames, lengths, offsets = bench.make_segments(torch, dev, n, 1234, word)
+fixed = int(os.environ.get("EWK_FIXED_LEN", "0"))   # > 0: every segment that many samples (T-sweep)
+pcm, off, ln, frames, lengths, offsets = bench.make_segments(torch, dev, n, 1234, word, fixed_len=fixed)
 if os.environ.get("EWK_SORT"):   # experiment: hand the kernel its work longest-first (LPT)
     order = torch.argsort(ln, descending=True)
     off, ln = off[order].contiguous(), ln[order].contiguous()
@@ -30,7 +31,7 @@ torch.cuda.synchronize()
 ms, k = e.profile_read(0)
 ms /= k
 lib = os.path.basename(os.environ.get("EWK_LIB", "libewk.so"))
-print(f"{lib:28s} {ms:8.3f} ms  {frames/ms/1e6:7.3f} Gframes/s  frac={frames*640/(ms/1e3)/8e12:.4f}  "
+print(f"{lib:28s} L={fixed or 'ragged'} {ms:8.3f} ms  {frames/ms/1e6:7.3f} Gframes/s  frac={frames*640/(ms/1e3)/8e12:.4f}  "
       f"matches={int(match.sum())} nan={int(torch.isnan(score).sum())} s0={float(score[0]):.4f}")
 import ctypes
 lib = ctypes.CDLL(os.environ.get("EWK_LIB") or os.path.join(ROOT, "easywakeword_amd", "libewk.so"))

@@ -61,3 +61,26 @@ def test_index_name_and_magic_words():
 def test_unmatched_spec_raises(spec):
     with pytest.raises(ValueError):
         ADM.select_device(spec, sd=stub())                            # no device has signal for "best"
+
+
+def test_no_input_device_is_an_oserror_for_the_facade(monkeypatch):
+    """No input device at all: select_device raises NoInputDeviceError (a ValueError); the
+    facade's default source turns it into the documented OSError hint."""
+    from easywakeword_amd import devices
+    from easywakeword_amd.wakeword import _default_source
+    sd = stub()
+    sd.query_devices = lambda: [d for d in DEVICES if d["max_input_channels"] == 0]
+    with pytest.raises(devices.NoInputDeviceError):
+        ADM.select_device(None, sd=sd)
+
+    def none(spec, sd=None):
+        raise devices.NoInputDeviceError("no audio input devices found")
+    monkeypatch.setattr(devices.AudioDeviceManager, "select_device", staticmethod(none))
+    with pytest.raises(OSError, match="ArraySource"):
+        _default_source(None)
+
+    def unmatched(spec, sd=None):
+        raise ValueError("no audio input device matches 'x'")
+    monkeypatch.setattr(devices.AudioDeviceManager, "select_device", staticmethod(unmatched))
+    with pytest.raises(ValueError, match="matches"):
+        _default_source("x")

@@ -95,6 +95,47 @@ def _worker_match(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _worker_match_ksteps(rank, world, port, q):
+    """K = 3 steps: per-step gathers vs one batched flush of three device-side adds."""
+    _init(rank, world, port)
+    try:
+        first, count = shard_streams(N_STREAMS, rank, world)
+        sc, mt = _score_streams(range(first, first + count))
+        steps = [(torch.from_numpy(sc + k), torch.from_numpy(np.roll(mt, k))) for k in range(3)]
+        g1 = MatchGather(len(sc), first * SEG_PER_STREAM, torch.device("cpu"))
+        per_step = [g1(s, m) for s, m in steps]
+        g3 = MatchGather(len(sc), first * SEG_PER_STREAM, torch.device("cpu"), steps=3)
+        for s, m in steps:
+            g3.add(s, m)
+        with pytest.raises(RuntimeError):
+            g3.add(*steps[0])
+        batched = g3.flush()
+        again = [g1(s, m) for s, m in steps[:1]]   # the buffer re-arms after a flush
+        q.put((rank, None if batched is None else (batched.numpy(), [p.numpy() for p in per_step],
+                                                    again[0].numpy())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_match_gather_k_steps_equals_per_step(world):
+    """A K-step batched gather (records held on the device, one flush) delivers exactly
+    the per-step gathers' records, each tagged with its step index."""
+    res = _run_world(_worker_match_ksteps, world)
+    batched, per_step, again = res[0]
+    assert all(res[r] is None for r in range(1, world))
+    want = []
+    for k, rec in enumerate(per_step):
+        r = rec.copy()
+        r[:, 2] = k
+        want.append(r)
+    # per rank: steps in order; ranks concatenated -> compare as sorted record sets and per step
+    got = sorted(map(tuple, batched.tolist()))
+    assert got == sorted(map(tuple, np.concatenate(want).tolist()))
+    assert len(batched) == sum(len(w) for w in want) > 0
+    np.testing.assert_array_equal(again, per_step[0])
+
+
 def test_shard_streams_partition():
     for n in (0, 1, 5, 1024, 8193):
         for world in (1, 2, 3, 8):
@@ -115,7 +156,7 @@ def test_gloo_match_gather_equals_single_process(world):
     ref_s, ref_m = _score_streams(range(N_STREAMS))
     assert ref_m.any() and not ref_m.all()     # both decisions occur
     idx = np.nonzero(ref_m)[0]
-    want = np.stack([idx.astype(np.int64), ref_s[idx].view(np.int64)], 1)
+    want = np.stack([idx.astype(np.int64), ref_s[idx].view(np.int64), np.zeros(len(idx), np.int64)], 1)
     np.testing.assert_array_equal(res[0], want)
     assert all(res[r] is None for r in range(1, world))
 
@@ -204,7 +245,7 @@ def _oracle_shard(streams, audio, on_tick):
         on_tick(np.array(rows, dtype=EVENT_DTYPE), seg)
 
 
-def _worker_stream(rank, world, port, q):
+def _worker_stream(rank, world, port, q, audio_cap=10000):
     _init(rank, world, port)
     try:
         from oracle.gate_ref import normalize_level3
@@ -213,12 +254,15 @@ def _worker_stream(rank, world, port, q):
         segs = {}
 
         def audio_fn(ev):
+            # only the segments of the tick just polled are readable (a compact ring
+            # overwrites older ones): the collector must capture PCM in add()
             return [torch.from_numpy(normalize_level3(segs[(int(e["stream"]), int(e["tick"]))])) for e in ev]
 
-        col = PositiveCollector(first, torch.device("cpu"), every=EVERY, audio_cap=10000, audio_fn=audio_fn)
+        col = PositiveCollector(first, torch.device("cpu"), every=EVERY, audio_cap=audio_cap, audio_fn=audio_fn)
         got_rec, got_aud = [], []
 
         def on_tick(ev, seg):
+            segs.clear()
             segs.update(seg)
             col.add(ev)
             rec, aud = col.tick()
@@ -234,6 +278,35 @@ def _worker_stream(rank, world, port, q):
         q.put((rank, (np.concatenate(got_rec), got_aud) if rank == 0 else (len(got_rec), len(got_aud))))
     finally:
         dist.destroy_process_group()
+
+
+def _worker_stream_cap2(rank, world, port, q):
+    _worker_stream(rank, world, port, q, audio_cap=1)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_streaming_positives_audio_cap(world):
+    """audio_cap = 1 per rank and flush: every positive's record arrives, the PCM rides with
+    the newest ones (captured at their poll) and matches each record it is paired with."""
+    from oracle.gate_ref import normalize_level3
+    res = _run_world(_worker_stream_cap2, world)
+    rec, aud = res[0]
+    audio = _stream_audio()
+    want_aud = {}
+
+    def on_tick(ev, seg):
+        for e in ev[(ev["match"] != 0) & ((ev["flags"] & 1) == 0)]:
+            key = (int(e["stream"]), int(e["tick"]))
+            want_aud[key] = normalize_level3(seg[key])
+
+    _oracle_shard(range(STREAMS_S), audio, on_tick)
+    assert sorted((r[0], r[1]) for r in rec.tolist()) == sorted(want_aud)
+    assert 0 < len(aud) <= len(rec)
+    # gather_positives pairs rank r's PCM with its first records: find each audio's record
+    # by length-order consistency -- every PCM equals the segment of some gathered record
+    keys = [(r[0], r[1]) for r in rec.tolist()]
+    for a in aud:
+        assert any(len(a) == len(want_aud[k]) and np.array_equal(a, want_aud[k]) for k in keys)
 
 
 @pytest.mark.parametrize("world", [2, 3])
