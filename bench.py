@@ -186,8 +186,14 @@ def cpu_baseline(host_pcm, lengths, offsets, seconds):
     frames = sum(r[0] for r in res)
     segs = sum(r[1] for r in res)
     wall = max(r[2] for r in res)
+    rates = np.array([r[0] / r[2] for r in res if r[2] > 0])   # each worker process's own rate
     return {"value": frames / wall, "unit": "frames/s", "cores": procs, "host_cores_affinity": aff,
             "cpu_quota_cores": quota, "kind": "port",
+            # per-core rate and its spread over the worker processes: the aggregate depends on
+            # how many cores the box's cgroup grants and how busy its other tenants keep them
+            "per_core": {"median": float(np.median(rates)), "min": float(rates.min()), "max": float(rates.max()),
+                         "spread_pct": float(100.0 * (rates.max() - rates.min()) / np.median(rates)),
+                         "unit": "frames/s per process"},
             "sample": f"{segs} segments ({frames} MFCC frames) of the same ragged batch, float64 candidate path, "
                       f"oracle/mfcc_ref.py (numpy/scipy restatement of librosa 0.11.0 mfcc + scipy cosine), "
                       f"{procs} processes x ~{seconds:.0f} s, OMP_NUM_THREADS=1"}
@@ -248,7 +254,11 @@ def cpu_stream_baseline(seconds, procs):
     with ctx.Pool(procs, initializer=_pool_init) as pool:
         res = pool.map(_cpu_stream_worker, [(9000 + p, seconds) for p in range(procs)])
     rtf = sum(t * 0.1 / w for t, w in res)       # seconds of audio per second, summed over processes
+    per = np.array([t * 0.1 / w for t, w in res])
     return {"value": rtf, "unit": "streams sustained in real time", "cores": procs, "kind": "port",
+            "per_core": {"median": float(np.median(per)), "min": float(per.min()), "max": float(per.max()),
+                         "spread_pct": float(100.0 * (per.max() - per.min()) / np.median(per)),
+                         "unit": "real-time streams per process"},
             "sample": f"{procs} processes x ~{seconds:.0f} s, each one synthetic stream of the streaming recipe "
                       f"through oracle/gate_ref.py DetectorRef (ring, block RMS, pct25, FSM, cut) + "
                       f"oracle/mfcc_ref.py level 2 per emitted segment, OMP_NUM_THREADS=1"}

@@ -50,7 +50,26 @@
 // s_setprio 1 over the frame-pass LDS phases (window, transposes, mel): -0.4 %
 #define EWK_SETPRIO(v) __builtin_amdgcn_s_setprio(v)
 
+// Per-wave phase timing of the linear-batch scorer (debug builds with -DEWK_TIMING only:
+// scripts/mb_score.py prints it; the product build compiles none of it).  dbg[k] sums the
+// s_memtime cycles of phase k over the wave's segments; the kernel adds them to g_ewk_dbg.
+#ifdef EWK_TIMING
+#define EWK_DBG_PARAM , uint64_t(&dbg)[12]
+#define EWK_DBG_ARG , dbg
+#define EWK_TS(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define EWK_TADD(k, a, b) dbg[k] += (b) - (a)
+#else
+#define EWK_DBG_PARAM
+#define EWK_DBG_ARG
+#define EWK_TS(v)
+#define EWK_TADD(k, a, b)
+#endif
+
 namespace ewk {
+
+#ifdef EWK_TIMING
+__device__ unsigned long long g_ewk_dbg[12];
+#endif
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
@@ -102,11 +121,13 @@ constexpr int DCT_RT1_STRIDE = 17 * 16;                   // 16 data chunks [l >
 constexpr int DCT_BYTES = DCT_RT1 + 8 * DCT_RT1_STRIDE;
 constexpr int L_SHARED_END = ((L_DCT + DCT_BYTES) + 15) & ~15;
 constexpr int W_TILE = 0;                                 // 16 frame rows x 512 B of f16 hi/lo chunks (tile_chunk)
-// per-tile record of the speculative top_db clamp (segment_stats): stored log-mel minima,
-// the clamps and the processing order (3 x kSpecTiles; tiles of frames 0..1023)
-constexpr int kSpecTiles = 64;
+// per-tile record of the speculative top_db clamp (segment_stats): stored log-mel minima per
+// pass, the clamps and the processing order ((passes per tile + 2) x kSpecTiles ints)
+constexpr int kSpecTiles = 48;   // tiles of frames 0..767 (7.7 s) are recorded and scout-ordered
 constexpr int W_SPEC = W_TILE + 16 * NMEL * 4;
-constexpr int W_BYTES = W_SPEC + 3 * kSpecTiles * 4;     // + the tile order (segment_stats)
+constexpr int kSpecRun = (16 / kFPP) * kSpecTiles;      // spec[kSpecRun + tile]: the tile's clamp
+constexpr int kSpecOrder = kSpecRun + kSpecTiles;        // spec[kSpecOrder + k]: k-th tile processed
+constexpr int W_BYTES = W_SPEC + (kSpecOrder + kSpecTiles) * 4;
 constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
 constexpr int LDS_BYTES = L_WG + 16 + 8 * WAVES;
 constexpr int kRescoreFrames = 16;
@@ -902,37 +923,48 @@ __device__ __forceinline__ void zero_rows(float* tile, int row0, int lane) {
 // theta in LDS the columns to add.  (Parking every tile in global memory for this pass
 // instead wrote 10 KB per 16 frames -- 2.3x the algorithmic traffic -- for the ~16 % of
 // bench tiles that need it; recomputing those costs the same time.)
+// Passes of one tile; `mask` bit p selects pass p (the others' rows are zeroed, like the
+// rows of frames past T).
+constexpr int kPassesPerTile = 16 / kFPP;
+constexpr int kAllPasses = (1 << kPassesPerTile) - 1;
 template <int RING>
 __device__ __forceinline__ void tile_passes(const SegSrc<RING>& v, int tile_i, int T, const unsigned char* smem,
                                             float* scr, float* tile, int lane, const int (&lo)[8], float& mx,
-                                            float& mn, float& nanp, float clampv) {
+                                            float& mn, float& nanp, float clampv, int mask = kAllPasses) {
     const int npass = (T + kFPP - 1) / kFPP;
-    {   // stage the tile's first pass
+    const int p0 = tile_i * kPassesPerTile;
+    mask &= npass - p0 >= kPassesPerTile ? kAllPasses : (1 << max(0, npass - p0)) - 1;
+    if (mask) {   // stage the tile's first selected pass
         float r[kStageLoads];
-        stage_load(v, tile_i * 16 * HOP - NFFT / 2, lane, r);
+        stage_load(v, (p0 + __builtin_ctz(mask)) * kFPP * HOP - NFFT / 2, lane, r);
         stage_store(scr, lane, r);
         lds_order();
     }
 #pragma unroll 1
-    for (int p = 0; p < 16 / kFPP; ++p) {
-        const int pass = tile_i * (16 / kFPP) + p;
-        if (pass < npass)
-            frame_pass(v, pass * kFPP, T, p * kFPP, p + 1 < 16 / kFPP && pass + 1 < npass ? (pass + 1) * kFPP : -1,
+    for (int p = 0; p < kPassesPerTile; ++p) {
+        if ((mask >> p) & 1) {
+            const int rest = mask >> (p + 1);   // the next selected pass of this tile is prefetched
+            frame_pass(v, (p0 + p) * kFPP, T, p * kFPP, rest ? (p0 + p + 1 + __builtin_ctz(rest)) * kFPP : -1,
                        smem, scr, tile, lane, lo, mx, mn, nanp, clampv);
-        else   // rows of frames past T: zero (ignored by the statistics)
+        } else {   // frames past T, or a pass left out: zero rows (their columns are not used)
             zero_rows(tile, p * kFPP, lane);
+        }
     }
     lds_order();
 }
 
+// The passes in `mask` of a tile whose stored values (clamped at `run`) include some below
+// the final threshold: recomputed bit for bit, their DCT columns swapped from clamped-at-run
+// to clamped-at-theta in the shifted sums.  A pass whose stored minimum is >= theta is
+// unchanged and skipped (per-pass records, segment_stats).
 template <int RING>
 __device__ __forceinline__ void fix_tile(const SegSrc<RING>& v, int tile_i, int T, float run, float theta,
                                          const unsigned char* smem, float* scr, float* tile, int lane,
                                          const int (&lo)[8], const float (&cref)[8], double (&s1)[8],
-                                         double (&s2)[8]) {
+                                         double (&s2)[8], int mask = kAllPasses) {
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     float d0 = 0.f, d1 = 0.f, d2 = 0.f;
-    tile_passes(v, tile_i, T, smem, scr, tile, lane, lo, d0, d1, d2, run);
+    tile_passes(v, tile_i, T, smem, scr, tile, lane, lo, d0, d1, d2, run, mask);
     float co[8], cn[8];
     tile_dct(tile, s_dct, lane, co);
     {
@@ -942,12 +974,14 @@ __device__ __forceinline__ void fix_tile(const SegSrc<RING>& v, int tile_i, int 
     }
     lds_order();
     tile_dct(tile, s_dct, lane, cn);
-    stats_replace(cn, co, cref, tile_i * 16 + (lane & 15) < T, s1, s2);
+    const int col = lane & 15;
+    stats_replace(cn, co, cref, tile_i * 16 + col < T && ((mask >> (col / kFPP)) & 1), s1, s2);
 }
 
 // Scout of a segment's tiles (tile t: frames 16t .. 16t + 15): the energy of 4 x 64 of its
 // samples (one 64-sample row every 640), wave-reduced; lane t returns the estimate for tile
 // t (t < ntile <= 64).  Only a processing-order heuristic: the results do not depend on it.
+constexpr int kScoutBatch = 8;   // tiles whose scout loads are in flight together
 template <int RING, int NB>
 __device__ __forceinline__ void scout_batch(const SegSrc<RING>& v, int t0, int lane, float& e) {
     float x[NB][4];
@@ -983,31 +1017,84 @@ __device__ __forceinline__ void scout_batch(const SegSrc<RING>& v, int t0, int l
 // samples (one 64-sample row every 640), wave-reduced; lane t returns the estimate for tile
 // t (t < ntile <= 64).  Only a processing-order heuristic: the results do not depend on it.
 // The loads of 8 tiles are in flight together (one memory round trip per 1.3 s of segment).
+// (scripts/scout_sim.py replays the order on the oracle's log-mel: this scout leaves ~7 % of
+// the bench's tiles to recompute, none with the true tile maxima; max-of-rows variants and
+// twice the loads reach 6.1 %.)
 template <int RING>
 __device__ __forceinline__ float scout_tiles(const SegSrc<RING>& v, int ntile, int lane) {
     float e = -1.0f;
-    for (int t0 = 0; t0 < ntile; t0 += 8) scout_batch<RING, 8>(v, t0, lane, e);
+    for (int t0 = 0; t0 < ntile; t0 += kScoutBatch) scout_batch<RING, kScoutBatch>(v, t0, lane, e);
     return e;
 }
 
+// The next work item of a persistent wave (linear batches, ring mode 2), claimed ahead:
+// its index is requested when the current segment's last tile starts, its work-order entry
+// when that tile's passes end and its descriptor before the fix-ups, so neither the atomic
+// nor the two dependent loads sit between two segments.  (Claiming at the segment start
+// instead holds a reservation for a whole segment and costs more at the batch tail.)
+struct WorkAhead {
+    int state = 0;      // 0 none, 1 index requested (lane 0), 2 index known, 3 described
+    int idx = 0;
+    int seg = 0;
+    int64_t start = 0;
+    int32_t len = 0;
+    int32_t stream = 0;
+    int32_t flags = 0;
+};
+struct WorkCtx {
+    const ScoreArgs* a;
+    int base, count;
+    bool ahead;         // claim the next item during this segment
+};
+
+template <int RING>
+__device__ __forceinline__ void work_claim(const WorkCtx& c, WorkAhead& w, int lane) {
+    if (lane == 0) w.idx = atomicAdd(c.a->work, 1);
+    w.state = 1;
+}
+template <int RING>
+__device__ __forceinline__ void work_order(const WorkCtx& c, WorkAhead& w) {
+    w.idx = __shfl(w.idx, 0, 64);
+    w.state = 2;
+    if (w.idx < c.count) w.seg = c.base + ((!RING && c.a->order) ? c.a->order[w.idx] : w.idx);
+}
+template <int RING>
+__device__ __forceinline__ void work_describe(const WorkCtx& c, WorkAhead& w) {
+    w.state = 3;
+    if (w.idx >= c.count) return;
+    if (RING) {
+        const ewk_event ev = c.a->events[w.seg];
+        w.start = ev.ring_start;
+        w.len = ev.length;
+        w.stream = ev.stream;
+        w.flags = ev.flags;
+    } else {
+        w.start = c.a->offsets[w.seg];
+        w.len = c.a->lengths[w.seg];
+    }
+}
+
 // Whole segment for one wave.  spec: this wave's per-tile record in LDS -- the stored
-// log-mel minimum of tile i in spec[i], its speculative clamp in spec[kSpecTiles + i]
-// (tiles past kSpecTiles are stored unclamped and always recomputed when theta bites),
-// then the processing order (kSpecTiles ints).
+// log-mel minimum of pass p of tile i in spec[kPassesPerTile * i + p], the tile's
+// speculative clamp in spec[kSpecRun + i] (tiles past kSpecTiles are stored unclamped and
+// always recomputed when theta bites), then the processing order (spec[kSpecOrder + k]).
 //
 // The top_db clamp (max - 80 dB over the whole segment) is applied speculatively at the
 // running max, which each tile updates before its DCT; a tile that already holds the
 // segment max needs no fix, so the tiles are processed loudest first by a scout estimate
-// (bench batch: 16 % of the tiles recomputed in time order, ~5 % in scout order).
+// (bench batch: 16 % of the tiles recomputed in time order, ~5 % in scout order), and only
+// the passes of a tile that hold a value below the final threshold are recomputed.
 template <int RING>
 __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, float* scr, float* tile,
-                              float* spec, int lane, const int (&lo)[8], double (&s1)[8], double (&s2)[8]) {
+                              float* spec, int lane, const int (&lo)[8], double (&s1)[8], double (&s2)[8],
+                              const WorkCtx& wc, WorkAhead& nx EWK_DBG_PARAM) {
+    EWK_TS(tq0);
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     const int T = 1 + v.len / HOP;
     const int ntile = (T + 15) >> 4;
     const int npass = (T + kFPP - 1) / kFPP;
     const int col = lane & 15;
-    int* order = reinterpret_cast<int*>(spec + 2 * kSpecTiles);
+    int* order = reinterpret_cast<int*>(spec + kSpecOrder);
     const bool ordered = ntile > 1 && ntile <= kSpecTiles;
     if (ordered) {   // loudest-first order: lane t ranks tile t (ties by index)
         float e = scout_tiles(v, ntile, lane);
@@ -1020,6 +1107,8 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         if (lane < ntile) order[rank] = lane;
         lds_order();
     }
+    EWK_TS(tq1);
+    EWK_TADD(1, tq0, tq1);
     float cref[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
@@ -1031,27 +1120,39 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         stage_store(scr, lane, r);
         lds_order();
     }
+    EWK_TS(tq2);
+    EWK_TADD(2, tq1, tq2);
     float run = -INFINITY;   // speculative clamp: running max - 80 dB
     for (int k = 0; k < ntile; ++k) {
+        EWK_TS(tk0);
         const int next_tile = k + 1 < ntile ? (ordered ? order[k + 1] : k + 1) : -1;
-        float tmin = INFINITY;
-        if (tile_i >= kSpecTiles) run = -INFINITY;
+        const bool rec = tile_i < kSpecTiles;
+        float tmw = INFINITY;
+        if (!rec) run = -INFINITY;
+        const bool last = k + 1 == ntile;
+        if (last && wc.ahead) work_claim<RING>(wc, nx, lane);
 #pragma unroll 1
-        for (int p = 0; p < 16 / kFPP; ++p) {
-            const int pass = tile_i * (16 / kFPP) + p;
+        for (int p = 0; p < kPassesPerTile; ++p) {
+            const int pass = tile_i * kPassesPerTile + p;
             // the next pass to prefetch: this tile's next, else the next tile's first
-            const int nxt = p + 1 < 16 / kFPP && pass + 1 < npass ? (pass + 1) * kFPP
-                                                                  : (next_tile >= 0 ? next_tile * 16 : -1);
+            const int nxt = p + 1 < kPassesPerTile && pass + 1 < npass ? (pass + 1) * kFPP
+                                                                      : (next_tile >= 0 ? next_tile * 16 : -1);
+            float tp = INFINITY;
             if (pass < npass)
-                frame_pass(v, pass * kFPP, T, p * kFPP, nxt, smem, scr, tile, lane, lo, vmax, tmin, nanp, run);
+                frame_pass(v, pass * kFPP, T, p * kFPP, nxt, smem, scr, tile, lane, lo, vmax, tp, nanp, run);
             else   // rows of frames past T: zero (ignored by the statistics)
                 zero_rows(tile, p * kFPP, lane);
+            const float tpw = wave_min(tp);   // this pass's minimum (its record below)
+            tmw = fminf(tmw, tpw);
+            if (lane == 0 && rec) spec[kPassesPerTile * tile_i + p] = tpw;
         }
         lds_order();
+        EWK_TS(tk1);
+        EWK_TADD(3, tk0, tk1);
+        if (last && wc.ahead) work_order<RING>(wc, nx);
         // max(max(x, run), final) = max(x, final): a tile stored clamped at the running max
         // (this tile's own values included) is exact unless a later tile raises the max
-        const float run2 = tile_i < kSpecTiles ? wave_max(vmax) - 80.0f : -INFINITY;
-        float tmw = wave_min(tmin);
+        const float run2 = rec ? wave_max(vmax) - 80.0f : -INFINITY;
         if (run2 > run && tmw < run2) {   // this tile raised the max over some of its own values
             uint4 h[4], l[4];
             clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
@@ -1067,9 +1168,18 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         }
         stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
         vmin = fminf(vmin, tmw);
-        if (lane == 0 && tile_i < kSpecTiles) { spec[tile_i] = fmaxf(tmw, run); spec[kSpecTiles + tile_i] = run; }
+        if (lane == 0 && rec) {   // stored minima: the pass minima as clamped at the tile's run
+#pragma unroll
+            for (int p = 0; p < kPassesPerTile; ++p)
+                spec[kPassesPerTile * tile_i + p] = fmaxf(spec[kPassesPerTile * tile_i + p], run);
+            spec[kSpecRun + tile_i] = run;
+        }
         tile_i = next_tile;
+        EWK_TS(tk2);
+        EWK_TADD(4, tk1, tk2);
     }
+    EWK_TS(tq3);
+    if (wc.ahead) work_describe<RING>(wc, nx);
     // wave-wide log-mel max
     vmax = wave_max(vmax);
     const float theta = vmax - 80.0f;
@@ -1077,16 +1187,30 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         lds_order();
         for (int cur = 0; cur < ntile; ++cur) {
             const bool rec = cur < kSpecTiles;
-            if (rec && !(spec[cur] < theta)) continue;
-            fix_tile(v, cur, T, rec ? spec[kSpecTiles + cur] : -INFINITY, theta, smem, scr, tile, lane, lo, cref, s1,
-                     s2);
+            int mask = kAllPasses;
+            if (rec) {   // only the passes holding a stored value below theta change
+                mask = 0;
+#pragma unroll
+                for (int p = 0; p < kPassesPerTile; ++p) mask |= (spec[kPassesPerTile * cur + p] < theta ? 1 : 0) << p;
+                if (!mask) continue;
+            }
+#ifdef EWK_TIMING
+            dbg[10] += 1;
+            dbg[11] += __builtin_popcount(mask);
+#endif
+            fix_tile(v, cur, T, rec ? spec[kSpecRun + cur] : -INFINITY, theta, smem, scr, tile, lane, lo, cref, s1,
+                     s2, mask);
         }
     }
     if (__ballot(nanp != nanp)) {   // NaN input: NaN statistics, NaN score (like the reference)
 #pragma unroll
         for (int i = 0; i < 8; ++i) s1[i] = __builtin_nan("");
     }
+    EWK_TS(tq4);
+    EWK_TADD(5, tq3, tq4);
     finish_stats(T, cref, s1, s2, lane, reinterpret_cast<double*>(scr));
+    EWK_TS(tq5);
+    EWK_TADD(6, tq4, tq5);
 }
 
 
@@ -1139,7 +1263,11 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
             for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
         }
         stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
-        if (lane == 0 && rec) { spec[lt] = fmaxf(tmw, run); spec[kSpecTiles + lt] = run; }
+        if (lane == 0 && rec) {   // tile-granular records (both passes recomputed when theta bites)
+#pragma unroll
+            for (int p = 0; p < kPassesPerTile; ++p) spec[kPassesPerTile * lt + p] = fmaxf(tmw, run);
+            spec[kSpecRun + lt] = run;
+        }
     }
     vmax = wave_max(vmax);
     if (lane == 0) { wg_mm[2 * wave] = vmax; wg_mm[2 * wave + 1] = vmin; }
@@ -1166,8 +1294,8 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
             lds_order();
             for (int lt = 0; lt + 1 < nloc; ++lt) {
                 const bool rec = lt < kSpecTiles;
-                if (rec && !(spec[lt] < theta)) continue;
-                fix_tile(v, wave + WAVES * lt, T, rec ? spec[kSpecTiles + lt] : -INFINITY, theta, smem, scr, tile,
+                if (rec && !(spec[kPassesPerTile * lt] < theta)) continue;
+                fix_tile(v, wave + WAVES * lt, T, rec ? spec[kSpecRun + lt] : -INFINITY, theta, smem, scr, tile,
                          lane, lo, cref, s1, s2);
             }
         }
@@ -1580,32 +1708,37 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
         ring_tick_end<RING>(a, smem, listed);
         return;
     }
+#ifdef EWK_TIMING
+    uint64_t dbg[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+    const WorkCtx wc = {&a, base, count, true};
+    WorkAhead nx;
     for (;;) {
-        int idx = 0;
-        if (lane == 0) idx = atomicAdd(a.work, 1);
-        idx = __shfl(idx, 0, 64);
-        if (idx >= count) break;
-        const int seg = base + ((!RING && a.order) ? a.order[idx] : idx);
-
-        int64_t start, ring = 0;
+        EWK_TS(tw0);
+        if (nx.state != 3) {   // nothing claimed ahead (first segment, or after a skipped event)
+            work_claim<RING>(wc, nx, lane);
+            work_order<RING>(wc, nx);
+            work_describe<RING>(wc, nx);
+        }
+        nx.state = 0;
+        if (nx.idx >= count) break;
+        const int seg = nx.seg;
+        int64_t ring = 0;
         const void* p;
-        int32_t len;
         if (RING) {
-            const ewk_event ev = a.events[seg];
-            if (ev.flags & EWK_EV_SKIPPED) continue;
-            p = static_cast<const unsigned char*>(ring_base) + (int64_t)ev.stream * a.ring_len * sample_bytes(RING);
-            start = ev.ring_start;
+            if (nx.flags & EWK_EV_SKIPPED) continue;
+            p = static_cast<const unsigned char*>(ring_base) + (int64_t)nx.stream * a.ring_len * sample_bytes(RING);
             ring = a.ring_len;
-            len = ev.length;
         } else {
             p = a.pcm;
-            start = a.offsets[seg];
-            len = a.lengths[seg];
         }
-        const SegSrc<RING> v = make_src<RING>(p, start, ring, len);
+        const SegSrc<RING> v = make_src<RING>(p, nx.start, ring, nx.len);
+        EWK_TS(tw1);
+        EWK_TADD(0, tw0, tw1);
 
         double st1[8], st2[8];
-        segment_stats(v, smem, scr, tile, spec, lane, lo, st1, st2);
+        segment_stats(v, smem, scr, tile, spec, lane, lo, st1, st2, wc, nx EWK_DBG_ARG);
+        EWK_TS(tw2);
 
         // ---- lane k < 20 holds coefficient k's mean / std (fp32-rounded like the reference's)
         const float cmf = act ? (float)st1[0] : 0.0f, csf = act ? (float)st2[0] : 0.0f;
@@ -1615,9 +1748,30 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
         }
         if (a.has_template) score_epilogue<RING>(a, cmf, csf, tmf, tsf, lane, seg, v.len, listed);
         lds_order();
+        EWK_TS(tw3);
+        EWK_TADD(7, tw2, tw3);
+#ifdef EWK_TIMING
+        dbg[9] += 1;
+#endif
     }   // work loop
+#ifdef EWK_TIMING
+    dbg[8] += 1;
+    if (lane == 0)
+        for (int k = 0; k < 12; ++k) atomicAdd(&g_ewk_dbg[k], (unsigned long long)dbg[k]);
+#endif
     if (RING) ring_tick_end<RING>(a, smem, listed);
 }
+
+#ifdef EWK_TIMING
+}  // namespace ewk
+extern "C" int ewk_debug_timing(unsigned long long* out) {   // read and reset (debug builds only)
+    unsigned long long z[12] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ewk::g_ewk_dbg), sizeof(z)) != hipSuccess) return -3;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(ewk::g_ewk_dbg), z, sizeof(z)) != hipSuccess) return -3;
+    return 0;
+}
+namespace ewk {
+#endif
 
 // Event-count snapshot taken on the gate's stream right after a gate launch: the
 // scoring pass that overlaps the next gate scores exactly the events of its own tick.

@@ -6,12 +6,17 @@ R="$(cd "$(dirname "$0")/.." && pwd)"
 REV=$1; NAME=$2; shift 2
 T=$(mktemp -d)
 mkdir -p "$T/easywakeword_amd/csrc" "$T/include" "$R/variants"
-for f in easywakeword_amd/csrc/ewk_mfcc.hip easywakeword_amd/csrc/ewk_gate.hip easywakeword_amd/csrc/ewk_level3.hip easywakeword_amd/csrc/ewk_engine.cpp \
-         easywakeword_amd/csrc/ewk_tables.cpp easywakeword_amd/csrc/ewk_internal.h easywakeword_amd/csrc/ewk_gate.h include/ewk.h; do
+SRCS="ewk_mfcc.hip ewk_gate.hip ewk_level3.hip ewk_engine.cpp ewk_tables.cpp"
+for f in easywakeword_amd/csrc/ewk_gather.hip; do   # sources that older revisions lack
+  if [ "$REV" = "WT" ] || git -C "$R" cat-file -e "$REV:$f" 2>/dev/null; then SRCS="$SRCS $(basename $f)"; fi
+done
+for s in $SRCS ewk_internal.h ewk_gate.h; do
+  f=easywakeword_amd/csrc/$s
   if [ "$REV" = "WT" ]; then cp "$R/$f" "$T/$f"; else git -C "$R" show "$REV:$f" > "$T/$f"; fi
 done
+if [ "$REV" = "WT" ]; then cp "$R/include/ewk.h" "$T/include/ewk.h"; else git -C "$R" show "$REV:include/ewk.h" > "$T/include/ewk.h"; fi
 objs=""
-for s in ewk_mfcc.hip ewk_gate.hip ewk_level3.hip ewk_engine.cpp ewk_tables.cpp; do
+for s in $SRCS; do
   x=""; [ "$s" = ewk_mfcc.hip ] && x="-fno-slp-vectorize"   # as easywakeword_amd/build.py EXTRA
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function $x "$@" \
      -c "$T/easywakeword_amd/csrc/$s" -o "$T/$s.o" &

@@ -35,14 +35,16 @@ print(f"{lib:28s} L={fixed or 'ragged'} {ms:8.3f} ms  {frames/ms/1e6:7.3f} Gfram
       f"matches={int(match.sum())} nan={int(torch.isnan(score).sum())} s0={float(score[0]):.4f}")
 import ctypes
 lib = ctypes.CDLL(os.environ.get("EWK_LIB") or os.path.join(ROOT, "easywakeword_amd", "libewk.so"))
-if hasattr(lib, "ewk_debug_timing"):
-    buf = (ctypes.c_ulonglong * 24)()
+if hasattr(lib, "ewk_debug_timing"):   # -DEWK_TIMING builds (easywakeword_amd/libewk_timing.so)
+    buf = (ctypes.c_ulonglong * 12)()
     lib.ewk_debug_timing(buf)      # reset
     e.profile(False)
     step(); torch.cuda.synchronize()
     lib.ewk_debug_timing(buf)
-    names = ["frame passes", "tile park+dct+stats", "clamp pass", "finish_stats", "fetch+setup", "epilogue", "wave lifetime"]
-    w = max(1, buf[7])
-    print("  per-wave cycles: " + ", ".join(f"{n}={buf[i] / w:,.0f}" for i, n in enumerate(names)))
-    sub = ["window", "prefetch issue", "dft1+tw", "transposes", "dft2", "untangle+power", "mel+log", "tile writes", "stage store"]
-    print("  frame-pass split: " + ", ".join(f"{n}={buf[8 + i] / w:,.0f}" for i, n in enumerate(sub)))
+    names = ["fetch+setup", "scout+rank", "first stage", "frame passes", "tile clamp/dct/stats", "recompute",
+             "finish_stats", "epilogue"]
+    waves, segs = max(1, buf[8]), max(1, buf[9])
+    tot = sum(buf[i] for i in range(8))
+    print(f"  waves={waves} segments={segs}; s_memtime cycles per segment: " +
+          ", ".join(f"{n}={buf[i] / segs:,.0f} ({100.0 * buf[i] / max(1, tot):.1f}%)" for i, n in enumerate(names)) +
+          f"; recomputed tiles/segment={buf[10] / segs:.3f} passes/segment={buf[11] / segs:.3f}")
