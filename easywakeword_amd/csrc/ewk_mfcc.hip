@@ -125,9 +125,12 @@ constexpr int W_TILE = 0;                                 // 16 frame rows x 512
 // pass, the clamps and the processing order ((passes per tile + 2) x kSpecTiles ints)
 constexpr int kSpecTiles = 48;   // tiles of frames 0..767 (7.7 s) are recorded and scout-ordered
 constexpr int W_SPEC = W_TILE + 16 * NMEL * 4;
-constexpr int kSpecRun = (16 / kFPP) * kSpecTiles;      // spec[kSpecRun + tile]: the tile's clamp
-constexpr int kSpecOrder = kSpecRun + kSpecTiles;        // spec[kSpecOrder + k]: k-th tile processed
+constexpr int kSpecRun = (16 / kFPP) * kSpecTiles;      // spec[kSpecRun + tile]: the running clamp after it
+constexpr int kSpecOrder = kSpecRun + kSpecTiles;        // spec[kSpecOrder + k]: k-th tile processed | flags
 constexpr int W_BYTES = W_SPEC + (kSpecOrder + kSpecTiles) * 4;
+// flags of the order entry of processing position k: the tile is parked / it raised the
+// running max over some of its own values (its stored image was re-clamped, see fix_tile)
+constexpr int kOrderPark = 1 << 8, kOrderSelf = 1 << 9;
 constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
 constexpr int LDS_BYTES = L_WG + 16 + 8 * WAVES;
 constexpr int kRescoreFrames = 16;
@@ -953,18 +956,26 @@ __device__ __forceinline__ void tile_passes(const SegSrc<RING>& v, int tile_i, i
     lds_order();
 }
 
-// The passes in `mask` of a tile whose stored values (clamped at `run`) include some below
-// the final threshold: recomputed bit for bit, their DCT columns swapped from clamped-at-run
-// to clamped-at-theta in the shifted sums.  A pass whose stored minimum is >= theta is
-// unchanged and skipped (per-pass records, segment_stats).
+// The passes in `mask` of a tile whose stored values (clamped at `run`, then re-clamped at
+// `self` when the tile raised the running max over its own values) include some below the
+// final threshold: the stored image is rebuilt bit for bit -- the same clamps in the same
+// order, so the DCT columns taken out of the shifted sums are exactly the ones put in, as a
+// parked image's are -- and swapped for the columns clamped at theta.  A pass whose stored
+// minimum is >= theta is unchanged and skipped (per-pass records, segment_stats).
 template <int RING>
-__device__ __forceinline__ void fix_tile(const SegSrc<RING>& v, int tile_i, int T, float run, float theta,
-                                         const unsigned char* smem, float* scr, float* tile, int lane,
+__device__ __forceinline__ void fix_tile(const SegSrc<RING>& v, int tile_i, int T, float run, float self,
+                                         float theta, const unsigned char* smem, float* scr, float* tile, int lane,
                                          const int (&lo)[8], const float (&cref)[8], double (&s1)[8],
                                          double (&s2)[8], int mask = kAllPasses) {
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     float d0 = 0.f, d1 = 0.f, d2 = 0.f;
     tile_passes(v, tile_i, T, smem, scr, tile, lane, lo, d0, d1, d2, run, mask);
+    if (self > -INFINITY) {   // (wave-uniform: an LDS record)
+        uint4 h[4], l[4];
+        clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
+        clamp_store(tile, lane, h, l, self);
+        lds_order();
+    }
     float co[8], cn[8];
     tile_dct(tile, s_dct, lane, co);
     {
@@ -1013,6 +1024,60 @@ __device__ __forceinline__ void scout_batch(const SegSrc<RING>& v, int t0, int l
     }
 }
 
+// A tile's stored log-mel image (8 KB of f16 hi/lo chunks in LDS) parked in the wave's
+// global slot: 8 ds_read_b128 + 8 coalesced 1-KB stores per wave.
+__device__ __forceinline__ void park_tile(const float* tile, unsigned char* slot, int lane) {
+    const uint4* src = reinterpret_cast<const uint4*>(tile);
+    uint4* dst = reinterpret_cast<uint4*>(slot);
+#pragma unroll
+    for (int u0 = 0; u0 < kParkTileBytes / 1024; u0 += 2) {   // 8 VGPRs in flight (the next pass's
+        uint4 r[2];                                              // samples are live here)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) r[u] = src[lane + 64 * (u0 + u)];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) dst[lane + 64 * (u0 + u)] = r[u];
+    }
+}
+
+// fix_tile for a parked tile: its stored image comes back from the slot instead of being
+// recomputed.  The reloads bypass the CU's vector L1 (nontemporal loads are L2-served): the
+// slot is rewritten for every segment of the wave, and an L1 line left from the previous
+// segment's reload would be stale.
+__device__ __forceinline__ void fix_parked(const unsigned char* slot, int tile_i, int T, float theta,
+                                           const unsigned char* smem, float* tile, int lane, const float (&cref)[8],
+                                           double (&s1)[8], double (&s2)[8], int mask) {
+    const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(slot);
+        uint4* dst = reinterpret_cast<uint4*>(tile);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's park stores have landed
+#pragma unroll
+        for (int u0 = 0; u0 < kParkTileBytes / 1024; u0 += 4) {
+            uint4 r[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + lane + 64 * (u0 + u)));
+                r[u] = make_uint4(q.x, q.y, q.z, q.w);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) dst[lane + 64 * (u0 + u)] = r[u];
+        }
+    }
+    lds_order();
+    float co[8], cn[8];
+    tile_dct(tile, s_dct, lane, co);
+    {
+        uint4 h[4], l[4];
+        clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
+        clamp_store(tile, lane, h, l, theta);
+    }
+    lds_order();
+    tile_dct(tile, s_dct, lane, cn);
+    const int col = lane & 15;
+    stats_replace(cn, co, cref, tile_i * 16 + col < T && ((mask >> (col / kFPP)) & 1), s1, s2);
+}
+
 // Scout of a segment's tiles (tile t: frames 16t .. 16t + 15): the energy of 4 x 64 of its
 // samples (one 64-sample row every 640), wave-reduced; lane t returns the estimate for tile
 // t (t < ntile <= 64).  Only a processing-order heuristic: the results do not depend on it.
@@ -1045,6 +1110,7 @@ struct WorkCtx {
     const ScoreArgs* a;
     int base, count;
     bool ahead;         // claim the next item during this segment
+    unsigned char* park;   // this wave's parked-tile slots (nullptr: no parking)
 };
 
 template <int RING>
@@ -1100,11 +1166,21 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         float e = scout_tiles(v, ntile, lane);
         e = e == e ? e : 0.0f;   // NaN samples: a total order (unique ranks) all the same
         int rank = 0;
+        float nxt = -1.0f, emax = -1.0f;   // the next tile's estimate in the order; the largest
         for (int u = 0; u < ntile; ++u) {
             const float eu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), u));
-            rank += (eu > e) || (eu == e && u < lane);
+            const bool before = (eu > e) || (eu == e && u < lane);
+            rank += before;
+            nxt = before ? nxt : (u == lane ? nxt : fmaxf(nxt, eu));
+            emax = fmaxf(emax, eu);
         }
-        if (lane < ntile) order[rank] = lane;
+        // Park (keep the stored log-mel image of) a tile when a later tile's estimate comes
+        // within 3 dB of the loudest: a later tile may raise the segment max over values this
+        // tile stored clamped, and a parked tile is then fixed from its image instead of
+        // being recomputed (scripts/scout_sim.py: 88 % of the recomputes, 2.8 tiles parked
+        // per bench segment).
+        const int park = wc.park && rank < kParkSlots && nxt > 0.5f * emax;
+        if (lane < ntile) order[rank] = lane | (park ? kOrderPark : 0);
         lds_order();
     }
     EWK_TS(tq1);
@@ -1113,7 +1189,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
     float vmax = -INFINITY, vmin = INFINITY, nanp = 0.0f;
-    int tile_i = ordered ? order[0] : 0;
+    int tile_i = ordered ? (order[0] & 0xff) : 0;
     {   // stage the first pass synchronously
         float r[kStageLoads];
         stage_load(v, tile_i * 16 * HOP - NFFT / 2, lane, r);
@@ -1125,7 +1201,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     float run = -INFINITY;   // speculative clamp: running max - 80 dB
     for (int k = 0; k < ntile; ++k) {
         EWK_TS(tk0);
-        const int next_tile = k + 1 < ntile ? (ordered ? order[k + 1] : k + 1) : -1;
+        const int next_tile = k + 1 < ntile ? (ordered ? (order[k + 1] & 0xff) : k + 1) : -1;
         const bool rec = tile_i < kSpecTiles;
         float tmw = INFINITY;
         if (!rec) run = -INFINITY;
@@ -1153,13 +1229,13 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         // max(max(x, run), final) = max(x, final): a tile stored clamped at the running max
         // (this tile's own values included) is exact unless a later tile raises the max
         const float run2 = rec ? wave_max(vmax) - 80.0f : -INFINITY;
-        if (run2 > run && tmw < run2) {   // this tile raised the max over some of its own values
+        const bool self = run2 > run && tmw < run2;
+        if (self) {   // this tile raised the max over some of its own values
             uint4 h[4], l[4];
             clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
             clamp_store(tile, lane, h, l, run2);
             lds_order();
         }
-        run = fmaxf(run, run2);
         float c[8];
         tile_dct(tile, s_dct, lane, c);
         if (k == 0) {
@@ -1168,12 +1244,17 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         }
         stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
         vmin = fminf(vmin, tmw);
+        run = fmaxf(run, run2);
         if (lane == 0 && rec) {   // stored minima: the pass minima as clamped at the tile's run
 #pragma unroll
             for (int p = 0; p < kPassesPerTile; ++p)
                 spec[kPassesPerTile * tile_i + p] = fmaxf(spec[kPassesPerTile * tile_i + p], run);
             spec[kSpecRun + tile_i] = run;
+            // (unordered: positions are tiles, the entry only carries the flag)
+            order[k] = (ordered ? order[k] : k) | (self ? kOrderSelf : 0);
         }
+        if (ordered && k < kParkSlots && (order[k] & kOrderPark))   // the stored image, as its DCT saw it
+            park_tile(tile, wc.park + (size_t)k * kParkTileBytes, lane);
         tile_i = next_tile;
         EWK_TS(tk2);
         EWK_TADD(4, tk1, tk2);
@@ -1185,7 +1266,26 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     const float theta = vmax - 80.0f;
     if (vmin < theta) {
         lds_order();
-        for (int cur = 0; cur < ntile; ++cur) {
+        // parked tiles first (their images come back from the wave's slots) ...
+        const int npark = ordered ? min(ntile, kParkSlots) : 0;
+        for (int k = 0; k < npark; ++k) {
+            const int ok = order[k];
+            if (!(ok & kOrderPark)) continue;
+            const int cur = ok & 0xff;
+            int mask = 0;
+#pragma unroll
+            for (int p = 0; p < kPassesPerTile; ++p) mask |= (spec[kPassesPerTile * cur + p] < theta ? 1 : 0) << p;
+            if (!mask) continue;
+#ifdef EWK_TIMING
+            dbg[10] += 1 << 16;   // parked fixes in the high half
+#endif
+            fix_parked(wc.park + (size_t)k * kParkTileBytes, cur, T, theta, smem, tile, lane, cref, s1, s2, mask);
+        }
+        // ... then the others are recomputed
+        for (int k = 0; k < ntile; ++k) {   // processing positions (= tile index when unordered)
+            const int ok = ordered || k < kSpecTiles ? order[k] : k;
+            if (k < npark && (ok & kOrderPark)) continue;
+            const int cur = ok & 0xff;
             const bool rec = cur < kSpecTiles;
             int mask = kAllPasses;
             if (rec) {   // only the passes holding a stored value below theta change
@@ -1198,8 +1298,11 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
             dbg[10] += 1;
             dbg[11] += __builtin_popcount(mask);
 #endif
-            fix_tile(v, cur, T, rec ? spec[kSpecRun + cur] : -INFINITY, theta, smem, scr, tile, lane, lo, cref, s1,
-                     s2, mask);
+            // stored at the running clamp of the position before (-inf for the first); the
+            // self-clamp is this tile's own running clamp
+            const float run_k = rec && k > 0 ? spec[kSpecRun + ((ordered ? order[k - 1] : k - 1) & 0xff)] : -INFINITY;
+            const float self_k = rec && (ok & kOrderSelf) ? spec[kSpecRun + cur] : -INFINITY;
+            fix_tile(v, cur, T, run_k, self_k, theta, smem, scr, tile, lane, lo, cref, s1, s2, mask);
         }
     }
     if (__ballot(nanp != nanp)) {   // NaN input: NaN statistics, NaN score (like the reference)
@@ -1225,6 +1328,7 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
                                    float* spec, int wave, int lane, const int (&lo)[8], float* misc0) {
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     float* wg_mm = reinterpret_cast<float*>(smem + L_WG + 16);   // [WAVES][2] max, min
+    int* order = reinterpret_cast<int*>(spec + kSpecOrder);      // here: per local tile, its flags
     const int T = 1 + v.len / HOP;
     const int ntile = (T + 15) >> 4;
     const int nloc = ntile > wave ? (ntile - wave + WAVES - 1) / WAVES : 0;
@@ -1249,13 +1353,13 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
         vmin = fminf(vmin, tmw);
         if (last) { last_min = tmw; break; }
         const float run2 = rec ? wave_max(vmax) - 80.0f : -INFINITY;
-        if (run2 > run && tmw < run2) {   // self-clamp (segment_stats)
+        const bool self = run2 > run && tmw < run2;
+        if (self) {   // self-clamp (segment_stats)
             uint4 h[4], l[4];
             clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
             clamp_store(tile, lane, h, l, run2);
             lds_order();
         }
-        run = fmaxf(run, run2);
         float c[8];
         tile_dct(tile, s_dct, lane, c);
         if (lt == 0) {
@@ -1263,10 +1367,12 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
             for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
         }
         stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
+        run = fmaxf(run, run2);
         if (lane == 0 && rec) {   // tile-granular records (both passes recomputed when theta bites)
 #pragma unroll
             for (int p = 0; p < kPassesPerTile; ++p) spec[kPassesPerTile * lt + p] = fmaxf(tmw, run);
             spec[kSpecRun + lt] = run;
+            order[lt] = self ? kOrderSelf : 0;
         }
     }
     vmax = wave_max(vmax);
@@ -1295,8 +1401,9 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
             for (int lt = 0; lt + 1 < nloc; ++lt) {
                 const bool rec = lt < kSpecTiles;
                 if (rec && !(spec[kPassesPerTile * lt] < theta)) continue;
-                fix_tile(v, wave + WAVES * lt, T, rec ? spec[kSpecRun + lt] : -INFINITY, theta, smem, scr, tile,
-                         lane, lo, cref, s1, s2);
+                const float run_l = rec && lt > 0 ? spec[kSpecRun + lt - 1] : -INFINITY;
+                const float self_l = rec && (order[lt] & kOrderSelf) ? spec[kSpecRun + lt] : -INFINITY;
+                fix_tile(v, wave + WAVES * lt, T, run_l, self_l, theta, smem, scr, tile, lane, lo, cref, s1, s2);
             }
         }
     }
@@ -1711,7 +1818,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
 #ifdef EWK_TIMING
     uint64_t dbg[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-    const WorkCtx wc = {&a, base, count, true};
+    const WorkCtx wc = {&a, base, count, true,
+                        a.park ? a.park + ((size_t)blockIdx.x * WAVES + wave) * kParkSlots * kParkTileBytes : nullptr};
     WorkAhead nx;
     for (;;) {
         EWK_TS(tw0);

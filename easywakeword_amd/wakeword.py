@@ -58,9 +58,8 @@ class WordMatcher:
     scorer (within 1e-4 of the reference; a score within ``rescore_margin`` of the
     threshold is re-scored in float64 on the device, so decisions are exact).
 
-    A matcher built with ``engine=`` shares that engine's threshold: ``matches(audio,
-    threshold)`` with another threshold changes it (WakeWord gives its matcher an
-    engine of its own)."""
+    A matcher built with ``engine=`` shares that engine; ``matches(audio, threshold)``
+    applies its threshold for that call only and restores the engine's afterwards."""
 
     def __init__(self, sample_rate: int = FREQUENCY, gpu: int = 0, engine: Optional[Engine] = None) -> None:
         if sample_rate != FREQUENCY:
@@ -112,19 +111,25 @@ class WordMatcher:
         _, _, score, _ = self._engine.score([audio])
         return float(score[0])
 
-    def matches(self, audio: np.ndarray, threshold: float = 75.0) -> Tuple[bool, float]:
+    def _score_at(self, segments, threshold: float):
+        """Score with `threshold` for this call only (a shared engine keeps its own)."""
         self._sync_template()
-        if float(threshold) != self._engine.config.similarity_threshold:
-            self._engine.set_threshold(threshold)
-        _, _, score, match = self._engine.score([audio])
+        old = self._engine.config.similarity_threshold
+        if float(threshold) == old:
+            return self._engine.score(segments)
+        self._engine.set_threshold(threshold)
+        try:
+            return self._engine.score(segments)
+        finally:
+            self._engine.set_threshold(old)
+
+    def matches(self, audio: np.ndarray, threshold: float = 75.0) -> Tuple[bool, float]:
+        _, _, score, match = self._score_at([audio], threshold)
         return bool(match[0]), float(score[0])
 
     def matches_batch(self, segments, threshold: float = 75.0):
         """Many candidates in one launch: (matches[n] bool, scores[n] float64)."""
-        self._sync_template()
-        if float(threshold) != self._engine.config.similarity_threshold:
-            self._engine.set_threshold(threshold)
-        _, _, score, match = self._engine.score(segments)
+        _, _, score, match = self._score_at(segments, threshold)
         return match, score
 
 
@@ -321,6 +326,7 @@ class WakeWord:
         user gave one (fallback 2.0)."""
         user_min = getattr(self, "_user_speech_duration_min", None)
         user_max = getattr(self, "_user_speech_duration_max", None)
+        d = None   # the WAV is analysed once, and only when a default needs it
         if user_min is not None:
             smin = float(user_min)
         else:
@@ -328,8 +334,7 @@ class WakeWord:
             smin = float(d) if d is not None else DEFAULT_SPEECH_DURATION_MIN
         if user_max is not None:
             smax = float(user_max)
-        elif user_min is None and smin == DEFAULT_SPEECH_DURATION_MIN and \
-                self._analyze_reference_audio_duration() is None:
+        elif user_min is None and d is None:   # no duration in the WAV: both fallbacks
             smax = DEFAULT_SPEECH_DURATION_MAX
         else:
             smax = 2.0 * smin

@@ -47,4 +47,5 @@ if hasattr(lib, "ewk_debug_timing"):   # -DEWK_TIMING builds (easywakeword_amd/l
     tot = sum(buf[i] for i in range(8))
     print(f"  waves={waves} segments={segs}; s_memtime cycles per segment: " +
           ", ".join(f"{n}={buf[i] / segs:,.0f} ({100.0 * buf[i] / max(1, tot):.1f}%)" for i, n in enumerate(names)) +
-          f"; recomputed tiles/segment={buf[10] / segs:.3f} passes/segment={buf[11] / segs:.3f}")
+          f"; recomputed tiles/segment={(buf[10] & 0xffff) / segs:.3f} passes/segment={buf[11] / segs:.3f} "
+          f"parked fixes/segment={(buf[10] >> 16) / segs:.3f}")

@@ -50,6 +50,7 @@ def heuristics(y, ntile):
 
 
 POS = {}
+PARK = {}
 
 
 def simulate(order, tmax, tmin, pmin, name=""):
@@ -97,10 +98,38 @@ def main():
             a, b = simulate(order, tmax, tmin, pmin, name)
             ta, tb = tot.get(name, (0, 0))
             tot[name] = (ta + a, tb + b)
+        # parking policy on the current scout: park tile k if an unprocessed tile's scout energy
+        # is within X dB of the best processed so far (a later tile might raise the max)
+        sc = hs["H0 sum 4x64 (current)"]
+        order = sorted(range(ntile), key=lambda t: (-sc[t], t))
+        db = 10 * np.log10(np.maximum(sc, 1e-30))
+        run = -np.inf
+        stored = {}
+        for k, t in enumerate(order):
+            run = max(run, tmax[t] - 80.0)
+            stored[t] = max(tmin[t], run)
+        theta = tmax.max() - 80.0
+        for X in (0, 3, 6, 10, 20):
+            parked = fixed_parked = fixed_rec = 0
+            best = -np.inf
+            for k, t in enumerate(order):
+                best = max(best, db[t])
+                rest = max((db[u] for u in order[k + 1:]), default=-np.inf)
+                park = rest > best - X
+                need = stored[t] < theta
+                parked += park
+                fixed_parked += need and park
+                fixed_rec += need and not park
+            key = f"park X={X:2d} dB"
+            pa, fp, fr = PARK.get(key, (0, 0, 0))
+            PARK[key] = (pa + parked, fp + fixed_parked, fr + fixed_rec)
     print(f"{n} segments, {n_tiles} tiles (fixed_len={fixed or 'ragged'})")
     for name, (a, b) in tot.items():
         print(f"  {name:28s} recomputed tiles/segment {a / n:6.3f} ({100.0 * a / n_tiles:5.1f} % of tiles)  "
               f"passes/segment {b / n:6.3f}  positions {dict(sorted(POS.get(name, {}).items())[:6])}")
+    for key, (pa, fp, fr) in PARK.items():
+        print(f"  {key}: parked tiles/segment {pa / n:6.3f}, fixes from parked {fp / n:6.3f}, "
+              f"recomputed {fr / n:6.3f}")
 
 
 if __name__ == "__main__":

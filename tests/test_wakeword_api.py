@@ -268,3 +268,22 @@ def test_waitforit_then_start_and_matcher_threshold_isolated():
     assert eng.config.reentry_timeout == 60.0                 # start(): re-entry every timeout s
     ww.stop()
     assert got[0] == "hello"
+
+
+@pytest.mark.gpu
+def test_shared_engine_threshold_is_per_call():
+    """WordMatcher(engine=shared).matches(x, threshold) applies the threshold to that call
+    and leaves the shared engine's own threshold as it was (VERDICT r2 weak #10)."""
+    import synth
+    from easywakeword_amd import Engine, WordMatcher
+    shared = Engine()
+    m = WordMatcher(engine=shared)
+    word = synth.load_word()
+    m.set_reference(word)
+    ok, s = m.matches(word, threshold=99.99)
+    assert s == 100.0 and ok                                # 100.0 >= 99.99
+    ok2, s2 = m.matches(word * np.float32(0.5), threshold=101.0)
+    assert not ok2
+    assert shared.config.similarity_threshold == 75.0
+    _, _, _, match = shared.score([word])
+    assert bool(match[0])
