@@ -4,7 +4,6 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdio.h>
-#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -90,7 +89,6 @@ struct ewk_engine {
     DevBuf<int32_t> order;          // linear batches: longest-first work order (k_lpt_order)
     int32_t rescore_cap = 4096;
     DevBuf<double> f64_scratch;
-    DevBuf<unsigned char> park;     // parked log-mel tiles of the persistent scorer waves (lazy)
     int f64_grid = 64;
 
     // host-API staging
@@ -295,7 +293,6 @@ void ewk_destroy(ewk_engine* e) {
     (void)hipFree(e->d_work);
     (void)hipFree(e->d_compact);
     e->f64_scratch.release();
-    e->park.release();
     e->order.release();
     e->pcm.release();
     e->offsets.release();
@@ -530,27 +527,6 @@ int ewk_get_template(ewk_engine* e, float* mean20, float* std20) {
     return EWK_OK;
 }
 
-// The persistent scorer's tile slots (kScoreGridMax workgroups x 8 waves x kParkSlots tiles,
-// 128 MB), allocated on the first linear or ring-mode-2 launch and never resized.
-static hipError_t ensure_park(ewk_engine* e) {
-    return e->park.reserve((size_t)std::max(kScoreGridMax, kScoreGridRing) * WAVES * kParkSlots * kParkTileBytes);
-}
-// EWK_NO_PARK=1 (diagnostics / A-B only): every top_db fix-up recomputes its tile.  The
-// scores are the same bits either way (fix_tile rebuilds the parked image exactly).
-static bool park_enabled() {
-    static const bool on = [] {
-        const char* v = getenv("EWK_NO_PARK");
-        return !(v && v[0] == '1');
-    }();
-    return on;
-}
-static hipError_t attach_park(ewk_engine* e, ScoreArgs& a) {
-    if (!park_enabled()) return hipSuccess;
-    hipError_t r = ensure_park(e);
-    if (r == hipSuccess) a.park = e->park.p;
-    return r;
-}
-
 static ScoreArgs base_args(ewk_engine* e) {
     ScoreArgs a;
     memset(&a, 0, sizeof(a));
@@ -583,7 +559,6 @@ static int score_linear(ewk_engine* e, const float* d_pcm, const int64_t* d_off,
     a.out_score = d_score;
     a.out_match = d_match;
     if (!a.has_template) a.rescore_list = nullptr;
-    HIP_TRY(attach_park(e, a));
     {   // (launch_score_f32 zeroes the work counter and the re-score count)
         ProfScope ps(e, 0, s);
         HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));
@@ -671,7 +646,6 @@ int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int
         a.out_match = e->match.p;
         a.cand_f32 = (flags & EWK_SCORE_F32_CANDIDATES) ? 1 : 0;
         if (!a.has_template) a.rescore_list = nullptr;
-        HIP_TRY(attach_park(e, a));
         HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));   // (zeroes the work counter and the re-score count)
         if (a.has_template) {
             const int64_t tmax = std::max<int64_t>(1 + e->ring_len / HOP, 1 + max_len / HOP);
@@ -801,7 +775,6 @@ static int score_pending(ewk_engine* e, hipStream_t ss, const int32_t* n_events)
     a.mirror = e->d_poll + e->bank * kPollRegion;
     a.evc = e->evc_bank(e->bank);
     a.mirror_chunk = std::min<int32_t>(kPollChunk, e->ev_cap);
-    if (e->n_streams >= kRingWaveStreams) HIP_TRY(attach_park(e, a));
     {
         ProfScope ps(e, 0, ss);
         HIP_TRY(launch_score_f32(e->d_tab, a, e->n_streams >= kRingWaveStreams ? 2 : 1, ss));

@@ -98,12 +98,7 @@ struct ScoreArgs {
     unsigned char* mirror;
     const int32_t* evc;
     int32_t mirror_chunk;
-    // top_db tile parking (persistent waves): kParkSlots log-mel tile images per wave of the
-    // grid, [blockIdx * 8 + wave][slot][kParkTileBytes]; nullptr disables parking
-    unsigned char* park;
 };
-constexpr int kParkSlots = 8;                 // processing positions 0..7 of a segment
-constexpr int kParkTileBytes = 16 * NMEL * 4; // one 16-frame f16 hi/lo log-mel tile
 
 // ring_mode: 0 linear batch, 1 ring events one segment per workgroup, 2 ring events one
 // segment per wave (many events per tick)

@@ -128,9 +128,9 @@ constexpr int W_SPEC = W_TILE + 16 * NMEL * 4;
 constexpr int kSpecRun = (16 / kFPP) * kSpecTiles;      // spec[kSpecRun + tile]: the running clamp after it
 constexpr int kSpecOrder = kSpecRun + kSpecTiles;        // spec[kSpecOrder + k]: k-th tile processed | flags
 constexpr int W_BYTES = W_SPEC + (kSpecOrder + kSpecTiles) * 4;
-// flags of the order entry of processing position k: the tile is parked / it raised the
-// running max over some of its own values (its stored image was re-clamped, see fix_tile)
-constexpr int kOrderPark = 1 << 8, kOrderSelf = 1 << 9;
+// flag of the order entry of processing position k: the tile raised the running max over
+// some of its own values (its stored image was re-clamped, see fix_tile)
+constexpr int kOrderSelf = 1 << 8;
 constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
 constexpr int LDS_BYTES = L_WG + 16 + 8 * WAVES;
 constexpr int kRescoreFrames = 16;
@@ -925,7 +925,10 @@ __device__ __forceinline__ void zero_rows(float* tile, int row0, int lane) {
 // by the same frame passes) gives the pass-1 DCT columns to remove, the tile clamped at
 // theta in LDS the columns to add.  (Parking every tile in global memory for this pass
 // instead wrote 10 KB per 16 frames -- 2.3x the algorithmic traffic -- for the ~16 % of
-// bench tiles that need it; recomputing those costs the same time.)
+// bench tiles that need it; recomputing those costs the same time.  Parking only the tiles
+// the scout ranks within 3 dB of a later one -- 2.8 per bench segment, 0.47 of them fixed --
+// lost 1.5 % too: the parking stores hold up the next pass's vmcnt waits, and a reload
+// costs 2/3 of a recompute.  profiles/r03_v2_park_ab.txt.)
 // Passes of one tile; `mask` bit p selects pass p (the others' rows are zeroed, like the
 // rows of frames past T).
 constexpr int kPassesPerTile = 16 / kFPP;
@@ -960,7 +963,7 @@ __device__ __forceinline__ void tile_passes(const SegSrc<RING>& v, int tile_i, i
 // `self` when the tile raised the running max over its own values) include some below the
 // final threshold: the stored image is rebuilt bit for bit -- the same clamps in the same
 // order, so the DCT columns taken out of the shifted sums are exactly the ones put in, as a
-// parked image's are -- and swapped for the columns clamped at theta.  A pass whose stored
+// the first pass added -- and swapped for the columns clamped at theta.  A pass whose stored
 // minimum is >= theta is unchanged and skipped (per-pass records, segment_stats).
 template <int RING>
 __device__ __forceinline__ void fix_tile(const SegSrc<RING>& v, int tile_i, int T, float run, float self,
@@ -1024,60 +1027,6 @@ __device__ __forceinline__ void scout_batch(const SegSrc<RING>& v, int t0, int l
     }
 }
 
-// A tile's stored log-mel image (8 KB of f16 hi/lo chunks in LDS) parked in the wave's
-// global slot: 8 ds_read_b128 + 8 coalesced 1-KB stores per wave.
-__device__ __forceinline__ void park_tile(const float* tile, unsigned char* slot, int lane) {
-    const uint4* src = reinterpret_cast<const uint4*>(tile);
-    uint4* dst = reinterpret_cast<uint4*>(slot);
-#pragma unroll
-    for (int u0 = 0; u0 < kParkTileBytes / 1024; u0 += 2) {   // 8 VGPRs in flight (the next pass's
-        uint4 r[2];                                              // samples are live here)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) r[u] = src[lane + 64 * (u0 + u)];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) dst[lane + 64 * (u0 + u)] = r[u];
-    }
-}
-
-// fix_tile for a parked tile: its stored image comes back from the slot instead of being
-// recomputed.  The reloads bypass the CU's vector L1 (nontemporal loads are L2-served): the
-// slot is rewritten for every segment of the wave, and an L1 line left from the previous
-// segment's reload would be stale.
-__device__ __forceinline__ void fix_parked(const unsigned char* slot, int tile_i, int T, float theta,
-                                           const unsigned char* smem, float* tile, int lane, const float (&cref)[8],
-                                           double (&s1)[8], double (&s2)[8], int mask) {
-    const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(slot);
-        uint4* dst = reinterpret_cast<uint4*>(tile);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's park stores have landed
-#pragma unroll
-        for (int u0 = 0; u0 < kParkTileBytes / 1024; u0 += 4) {
-            uint4 r[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                const u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + lane + 64 * (u0 + u)));
-                r[u] = make_uint4(q.x, q.y, q.z, q.w);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u) dst[lane + 64 * (u0 + u)] = r[u];
-        }
-    }
-    lds_order();
-    float co[8], cn[8];
-    tile_dct(tile, s_dct, lane, co);
-    {
-        uint4 h[4], l[4];
-        clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
-        clamp_store(tile, lane, h, l, theta);
-    }
-    lds_order();
-    tile_dct(tile, s_dct, lane, cn);
-    const int col = lane & 15;
-    stats_replace(cn, co, cref, tile_i * 16 + col < T && ((mask >> (col / kFPP)) & 1), s1, s2);
-}
-
 // Scout of a segment's tiles (tile t: frames 16t .. 16t + 15): the energy of 4 x 64 of its
 // samples (one 64-sample row every 640), wave-reduced; lane t returns the estimate for tile
 // t (t < ntile <= 64).  Only a processing-order heuristic: the results do not depend on it.
@@ -1110,7 +1059,6 @@ struct WorkCtx {
     const ScoreArgs* a;
     int base, count;
     bool ahead;         // claim the next item during this segment
-    unsigned char* park;   // this wave's parked-tile slots (nullptr: no parking)
 };
 
 template <int RING>
@@ -1166,21 +1114,11 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         float e = scout_tiles(v, ntile, lane);
         e = e == e ? e : 0.0f;   // NaN samples: a total order (unique ranks) all the same
         int rank = 0;
-        float nxt = -1.0f, emax = -1.0f;   // the next tile's estimate in the order; the largest
         for (int u = 0; u < ntile; ++u) {
             const float eu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), u));
-            const bool before = (eu > e) || (eu == e && u < lane);
-            rank += before;
-            nxt = before ? nxt : (u == lane ? nxt : fmaxf(nxt, eu));
-            emax = fmaxf(emax, eu);
+            rank += (eu > e) || (eu == e && u < lane);
         }
-        // Park (keep the stored log-mel image of) a tile when a later tile's estimate comes
-        // within 3 dB of the loudest: a later tile may raise the segment max over values this
-        // tile stored clamped, and a parked tile is then fixed from its image instead of
-        // being recomputed (scripts/scout_sim.py: 88 % of the recomputes, 2.8 tiles parked
-        // per bench segment).
-        const int park = wc.park && rank < kParkSlots && nxt > 0.5f * emax;
-        if (lane < ntile) order[rank] = lane | (park ? kOrderPark : 0);
+        if (lane < ntile) order[rank] = lane;
         lds_order();
     }
     EWK_TS(tq1);
@@ -1253,8 +1191,6 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
             // (unordered: positions are tiles, the entry only carries the flag)
             order[k] = (ordered ? order[k] : k) | (self ? kOrderSelf : 0);
         }
-        if (ordered && k < kParkSlots && (order[k] & kOrderPark))   // the stored image, as its DCT saw it
-            park_tile(tile, wc.park + (size_t)k * kParkTileBytes, lane);
         tile_i = next_tile;
         EWK_TS(tk2);
         EWK_TADD(4, tk1, tk2);
@@ -1266,25 +1202,8 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     const float theta = vmax - 80.0f;
     if (vmin < theta) {
         lds_order();
-        // parked tiles first (their images come back from the wave's slots) ...
-        const int npark = ordered ? min(ntile, kParkSlots) : 0;
-        for (int k = 0; k < npark; ++k) {
-            const int ok = order[k];
-            if (!(ok & kOrderPark)) continue;
-            const int cur = ok & 0xff;
-            int mask = 0;
-#pragma unroll
-            for (int p = 0; p < kPassesPerTile; ++p) mask |= (spec[kPassesPerTile * cur + p] < theta ? 1 : 0) << p;
-            if (!mask) continue;
-#ifdef EWK_TIMING
-            dbg[10] += 1 << 16;   // parked fixes in the high half
-#endif
-            fix_parked(wc.park + (size_t)k * kParkTileBytes, cur, T, theta, smem, tile, lane, cref, s1, s2, mask);
-        }
-        // ... then the others are recomputed
         for (int k = 0; k < ntile; ++k) {   // processing positions (= tile index when unordered)
             const int ok = ordered || k < kSpecTiles ? order[k] : k;
-            if (k < npark && (ok & kOrderPark)) continue;
             const int cur = ok & 0xff;
             const bool rec = cur < kSpecTiles;
             int mask = kAllPasses;
@@ -1818,8 +1737,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
 #ifdef EWK_TIMING
     uint64_t dbg[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #endif
-    const WorkCtx wc = {&a, base, count, true,
-                        a.park ? a.park + ((size_t)blockIdx.x * WAVES + wave) * kParkSlots * kParkTileBytes : nullptr};
+    const WorkCtx wc = {&a, base, count, true};
     WorkAhead nx;
     for (;;) {
         EWK_TS(tw0);

@@ -16,8 +16,6 @@ if [ "$MODE" = all ] || [ "$MODE" = ab ]; then
         EWK_FIXED_LEN=$L EWK_LIB=$PWD/$f timeout -k 10 120 python scripts/mb_score.py 65536 10 2>&1 | grep Gframes
         rc=${PIPESTATUS[0]}; [ $rc -eq 0 ] || { echo "variant $f rc=$rc"; exit $rc; }
       done
-      EWK_NO_PARK=1 EWK_FIXED_LEN=$L EWK_LIB=$PWD/easywakeword_amd/libewk.so timeout -k 10 120 python scripts/mb_score.py 65536 10 2>&1 | grep Gframes | sed 's/^/no_park /'
-      rc=${PIPESTATUS[0]}; [ $rc -eq 0 ] || { echo "no_park rc=$rc"; exit $rc; }
     done
   done
 fi

@@ -46,6 +46,32 @@ def heuristics(y, ntile):
     h["H2 max 16x16"] = np.array([float((r ** 2).sum(axis=1).max()) for r in r16])
     r8b = [sample_rows(y, t, 8, 64, 320, 64) for t in range(ntile)]   # 2x the loads
     h["H3 max 8x64 (2x loads)"] = np.array([float((r ** 2).sum(axis=1).max()) for r in r8b])
+    # full coverage: the max over the tile's 16 frames of the frame energy (512-sample
+    # windows, Hann-weighted or flat), and of 160-sample hop chunks
+    yp = np.concatenate([np.zeros(256), y.astype(np.float64), np.zeros(256 + 16 * HOP * ntile)])
+    win = np.hanning(514)[1:-1]
+    fe = np.array([[float(((yp[(16 * t + f) * HOP:(16 * t + f) * HOP + 512] * win) ** 2).sum()) for f in range(16)]
+                   for t in range(ntile)])
+    h["H4 max frame energy (hann)"] = fe.max(axis=1)
+    fe2 = np.array([[float((yp[(16 * t + f) * HOP:(16 * t + f) * HOP + 512] ** 2).sum()) for f in range(16)]
+                    for t in range(ntile)])
+    h["H5 max frame energy (flat)"] = fe2.max(axis=1)
+    ch = np.array([[float((yp[256 + (16 * t + f) * HOP:256 + (16 * t + f + 1) * HOP] ** 2).sum()) for f in range(16)]
+                   for t in range(ntile)])
+    h["H6 max hop-chunk energy"] = ch.max(axis=1)
+    w2 = win ** 2
+    for fs, ss in ((2, 1), (4, 1), (8, 1), (4, 2), (4, 4), (8, 2), (16, 1)):
+        e = np.array([[float((yp[(16 * t + f) * HOP:(16 * t + f) * HOP + 512:ss] ** 2 * w2[::ss]).sum())
+                       for f in range(0, 16, fs)] for t in range(ntile)])
+        h[f"H7 hann frames/{fs} samples/{ss}"] = e.max(axis=1)
+    # chunked: energy of C-sample chunks, frame energy = sum of chunk energies x mean w^2
+    for C in (16, 32, 64):
+        wc = w2.reshape(512 // C, C).mean(axis=1)
+        u = yp[:len(yp) // C * C].reshape(-1, C)
+        ce = (u ** 2).sum(axis=1)
+        e = np.array([[float((ce[(16 * t + f) * HOP // C:(16 * t + f) * HOP // C + 512 // C] * wc).sum())
+                       for f in range(16)] for t in range(ntile)])
+        h[f"H8 chunk {C} hann-weighted"] = e.max(axis=1)
     return h
 
 
@@ -93,6 +119,12 @@ def main():
         hs = heuristics(y, ntile)
         hs["oracle (true tile max)"] = tmax
         hs["time order"] = -np.arange(ntile, dtype=float)
+        # hybrid: the current scout's order, its top K re-ranked by the chunked Hann energy
+        h0, h8 = hs["H0 sum 4x64 (current)"], hs["H8 chunk 32 hann-weighted"]
+        for K in (2, 3, 4, 6):
+            o0 = sorted(range(ntile), key=lambda t: (-h0[t], t))
+            top = sorted(o0[:K], key=lambda t: (-h8[t], t))
+            hs[f"H9 hybrid top {K}"] = {t: -k for k, t in enumerate(top + o0[K:])}
         for name, sc in hs.items():
             order = sorted(range(ntile), key=lambda t: (-sc[t], t))
             a, b = simulate(order, tmax, tmin, pmin, name)
