@@ -125,12 +125,9 @@ constexpr int W_TILE = 0;                                 // 16 frame rows x 512
 // pass, the clamps and the processing order ((passes per tile + 2) x kSpecTiles ints)
 constexpr int kSpecTiles = 48;   // tiles of frames 0..767 (7.7 s) are recorded and scout-ordered
 constexpr int W_SPEC = W_TILE + 16 * NMEL * 4;
-constexpr int kSpecRun = (16 / kFPP) * kSpecTiles;      // spec[kSpecRun + tile]: the running clamp after it
-constexpr int kSpecOrder = kSpecRun + kSpecTiles;        // spec[kSpecOrder + k]: k-th tile processed | flags
+constexpr int kSpecRun = (16 / kFPP) * kSpecTiles;      // spec[kSpecRun + tile]: the tile's clamp
+constexpr int kSpecOrder = kSpecRun + kSpecTiles;        // spec[kSpecOrder + k]: k-th tile processed
 constexpr int W_BYTES = W_SPEC + (kSpecOrder + kSpecTiles) * 4;
-// flag of the order entry of processing position k: the tile raised the running max over
-// some of its own values (its stored image was re-clamped, see fix_tile)
-constexpr int kOrderSelf = 1 << 8;
 constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
 constexpr int LDS_BYTES = L_WG + 16 + 8 * WAVES;
 constexpr int kRescoreFrames = 16;
@@ -928,7 +925,12 @@ __device__ __forceinline__ void zero_rows(float* tile, int row0, int lane) {
 // bench tiles that need it; recomputing those costs the same time.  Parking only the tiles
 // the scout ranks within 3 dB of a later one -- 2.8 per bench segment, 0.47 of them fixed --
 // lost 1.5 % too: the parking stores hold up the next pass's vmcnt waits, and a reload
-// costs 2/3 of a recompute.  profiles/r03_v2_park_ab.txt.)
+// costs 2/3 of a recompute.  profiles/r03_v2_park_ab.txt.  Rebuilding a self-clamped tile's
+// stored image exactly -- its clamp at the run before it, then at its own -- so that the
+// columns taken out equal the ones put in to the last bit cost 1.3 %, for score changes of
+// ~1e-9: the fix-up recomputes at the tile's final run.  A full-coverage scout (Hann-weighted
+// frame energies from every sample, scripts/scout_sim.py H8) cut the recomputes from 0.53 to
+// 0.11 tiles per bench segment but its loads cost 4x the time saved: r03_v3_scout_ab.txt.)
 // Passes of one tile; `mask` bit p selects pass p (the others' rows are zeroed, like the
 // rows of frames past T).
 constexpr int kPassesPerTile = 16 / kFPP;
@@ -959,26 +961,18 @@ __device__ __forceinline__ void tile_passes(const SegSrc<RING>& v, int tile_i, i
     lds_order();
 }
 
-// The passes in `mask` of a tile whose stored values (clamped at `run`, then re-clamped at
-// `self` when the tile raised the running max over its own values) include some below the
-// final threshold: the stored image is rebuilt bit for bit -- the same clamps in the same
-// order, so the DCT columns taken out of the shifted sums are exactly the ones put in, as a
-// the first pass added -- and swapped for the columns clamped at theta.  A pass whose stored
-// minimum is >= theta is unchanged and skipped (per-pass records, segment_stats).
+// The passes in `mask` of a tile whose stored values (clamped at `run`) include some below
+// the final threshold: recomputed bit for bit, their DCT columns swapped from clamped-at-run
+// to clamped-at-theta in the shifted sums.  A pass whose stored minimum is >= theta is
+// unchanged and skipped (per-pass records, segment_stats).
 template <int RING>
-__device__ __forceinline__ void fix_tile(const SegSrc<RING>& v, int tile_i, int T, float run, float self,
-                                         float theta, const unsigned char* smem, float* scr, float* tile, int lane,
+__device__ __forceinline__ void fix_tile(const SegSrc<RING>& v, int tile_i, int T, float run, float theta,
+                                         const unsigned char* smem, float* scr, float* tile, int lane,
                                          const int (&lo)[8], const float (&cref)[8], double (&s1)[8],
                                          double (&s2)[8], int mask = kAllPasses) {
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     float d0 = 0.f, d1 = 0.f, d2 = 0.f;
     tile_passes(v, tile_i, T, smem, scr, tile, lane, lo, d0, d1, d2, run, mask);
-    if (self > -INFINITY) {   // (wave-uniform: an LDS record)
-        uint4 h[4], l[4];
-        clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
-        clamp_store(tile, lane, h, l, self);
-        lds_order();
-    }
     float co[8], cn[8];
     tile_dct(tile, s_dct, lane, co);
     {
@@ -1127,7 +1121,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
     float vmax = -INFINITY, vmin = INFINITY, nanp = 0.0f;
-    int tile_i = ordered ? (order[0] & 0xff) : 0;
+    int tile_i = ordered ? order[0] : 0;
     {   // stage the first pass synchronously
         float r[kStageLoads];
         stage_load(v, tile_i * 16 * HOP - NFFT / 2, lane, r);
@@ -1139,7 +1133,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     float run = -INFINITY;   // speculative clamp: running max - 80 dB
     for (int k = 0; k < ntile; ++k) {
         EWK_TS(tk0);
-        const int next_tile = k + 1 < ntile ? (ordered ? (order[k + 1] & 0xff) : k + 1) : -1;
+        const int next_tile = k + 1 < ntile ? (ordered ? order[k + 1] : k + 1) : -1;
         const bool rec = tile_i < kSpecTiles;
         float tmw = INFINITY;
         if (!rec) run = -INFINITY;
@@ -1167,13 +1161,13 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         // max(max(x, run), final) = max(x, final): a tile stored clamped at the running max
         // (this tile's own values included) is exact unless a later tile raises the max
         const float run2 = rec ? wave_max(vmax) - 80.0f : -INFINITY;
-        const bool self = run2 > run && tmw < run2;
-        if (self) {   // this tile raised the max over some of its own values
+        if (run2 > run && tmw < run2) {   // this tile raised the max over some of its own values
             uint4 h[4], l[4];
             clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
             clamp_store(tile, lane, h, l, run2);
             lds_order();
         }
+        run = fmaxf(run, run2);
         float c[8];
         tile_dct(tile, s_dct, lane, c);
         if (k == 0) {
@@ -1182,14 +1176,11 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         }
         stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
         vmin = fminf(vmin, tmw);
-        run = fmaxf(run, run2);
         if (lane == 0 && rec) {   // stored minima: the pass minima as clamped at the tile's run
 #pragma unroll
             for (int p = 0; p < kPassesPerTile; ++p)
                 spec[kPassesPerTile * tile_i + p] = fmaxf(spec[kPassesPerTile * tile_i + p], run);
             spec[kSpecRun + tile_i] = run;
-            // (unordered: positions are tiles, the entry only carries the flag)
-            order[k] = (ordered ? order[k] : k) | (self ? kOrderSelf : 0);
         }
         tile_i = next_tile;
         EWK_TS(tk2);
@@ -1202,9 +1193,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     const float theta = vmax - 80.0f;
     if (vmin < theta) {
         lds_order();
-        for (int k = 0; k < ntile; ++k) {   // processing positions (= tile index when unordered)
-            const int ok = ordered || k < kSpecTiles ? order[k] : k;
-            const int cur = ok & 0xff;
+        for (int cur = 0; cur < ntile; ++cur) {
             const bool rec = cur < kSpecTiles;
             int mask = kAllPasses;
             if (rec) {   // only the passes holding a stored value below theta change
@@ -1217,11 +1206,8 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
             dbg[10] += 1;
             dbg[11] += __builtin_popcount(mask);
 #endif
-            // stored at the running clamp of the position before (-inf for the first); the
-            // self-clamp is this tile's own running clamp
-            const float run_k = rec && k > 0 ? spec[kSpecRun + ((ordered ? order[k - 1] : k - 1) & 0xff)] : -INFINITY;
-            const float self_k = rec && (ok & kOrderSelf) ? spec[kSpecRun + cur] : -INFINITY;
-            fix_tile(v, cur, T, run_k, self_k, theta, smem, scr, tile, lane, lo, cref, s1, s2, mask);
+            fix_tile(v, cur, T, rec ? spec[kSpecRun + cur] : -INFINITY, theta, smem, scr, tile, lane, lo, cref, s1,
+                     s2, mask);
         }
     }
     if (__ballot(nanp != nanp)) {   // NaN input: NaN statistics, NaN score (like the reference)
@@ -1247,7 +1233,6 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
                                    float* spec, int wave, int lane, const int (&lo)[8], float* misc0) {
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     float* wg_mm = reinterpret_cast<float*>(smem + L_WG + 16);   // [WAVES][2] max, min
-    int* order = reinterpret_cast<int*>(spec + kSpecOrder);      // here: per local tile, its flags
     const int T = 1 + v.len / HOP;
     const int ntile = (T + 15) >> 4;
     const int nloc = ntile > wave ? (ntile - wave + WAVES - 1) / WAVES : 0;
@@ -1272,13 +1257,13 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
         vmin = fminf(vmin, tmw);
         if (last) { last_min = tmw; break; }
         const float run2 = rec ? wave_max(vmax) - 80.0f : -INFINITY;
-        const bool self = run2 > run && tmw < run2;
-        if (self) {   // self-clamp (segment_stats)
+        if (run2 > run && tmw < run2) {   // self-clamp (segment_stats)
             uint4 h[4], l[4];
             clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
             clamp_store(tile, lane, h, l, run2);
             lds_order();
         }
+        run = fmaxf(run, run2);
         float c[8];
         tile_dct(tile, s_dct, lane, c);
         if (lt == 0) {
@@ -1286,12 +1271,10 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
             for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
         }
         stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
-        run = fmaxf(run, run2);
         if (lane == 0 && rec) {   // tile-granular records (both passes recomputed when theta bites)
 #pragma unroll
             for (int p = 0; p < kPassesPerTile; ++p) spec[kPassesPerTile * lt + p] = fmaxf(tmw, run);
             spec[kSpecRun + lt] = run;
-            order[lt] = self ? kOrderSelf : 0;
         }
     }
     vmax = wave_max(vmax);
@@ -1320,9 +1303,8 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
             for (int lt = 0; lt + 1 < nloc; ++lt) {
                 const bool rec = lt < kSpecTiles;
                 if (rec && !(spec[kPassesPerTile * lt] < theta)) continue;
-                const float run_l = rec && lt > 0 ? spec[kSpecRun + lt - 1] : -INFINITY;
-                const float self_l = rec && (order[lt] & kOrderSelf) ? spec[kSpecRun + lt] : -INFINITY;
-                fix_tile(v, wave + WAVES * lt, T, run_l, self_l, theta, smem, scr, tile, lane, lo, cref, s1, s2);
+                fix_tile(v, wave + WAVES * lt, T, rec ? spec[kSpecRun + lt] : -INFINITY, theta, smem, scr, tile,
+                         lane, lo, cref, s1, s2);
             }
         }
     }
