@@ -9,7 +9,7 @@ if [ "$MODE" = all ] || [ "$MODE" = test ]; then
   rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.log
   [ $rc -eq 0 ] || exit $rc
 fi
-if [ "$MODE" = all ] || [ "$MODE" = ab ]; then
+if [ "$MODE" = all ] || [ "$MODE" = ab ] || [ "$MODE" = abt ]; then
   for r in 1 2; do
     for L in 0 16000; do
       for f in variants/*.so; do
@@ -19,6 +19,6 @@ if [ "$MODE" = all ] || [ "$MODE" = ab ]; then
     done
   done
 fi
-if [ "$MODE" = all ] || [ "$MODE" = timing ]; then
+if [ "$MODE" = all ] || [ "$MODE" = timing ] || [ "$MODE" = abt ]; then
   bash scripts/gpu_timing.sh
 fi
