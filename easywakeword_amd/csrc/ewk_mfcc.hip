@@ -54,21 +54,27 @@
 // scripts/mb_score.py prints it; the product build compiles none of it).  dbg[k] sums the
 // s_memtime cycles of phase k over the wave's segments; the kernel adds them to g_ewk_dbg.
 #ifdef EWK_TIMING
-#define EWK_DBG_PARAM , uint64_t(&dbg)[12]
+#define EWK_DBG_PARAM , uint64_t(&dbg)[kDbgN]
 #define EWK_DBG_ARG , dbg
 #define EWK_TS(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define EWK_TADD(k, a, b) dbg[k] += (b) - (a)
+// frame-pass sub-phases (dbg[12..18]) and passes timed (dbg[19]); tile_passes passes nullptr
+#define EWK_PASS_PARAM , uint64_t* pdbg
+#define EWK_PASS_ARG(x) , x
 #else
 #define EWK_DBG_PARAM
 #define EWK_DBG_ARG
 #define EWK_TS(v)
 #define EWK_TADD(k, a, b)
+#define EWK_PASS_PARAM
+#define EWK_PASS_ARG(x)
 #endif
+constexpr int kDbgN = 20;
 
 namespace ewk {
 
 #ifdef EWK_TIMING
-__device__ unsigned long long g_ewk_dbg[12];
+__device__ unsigned long long g_ewk_dbg[kDbgN];
 #endif
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
@@ -453,7 +459,8 @@ template <int RING>
 __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T, int row0, int next_t0,
                                            const unsigned char* smem, float* scr, float* tile,
                                            int lane, const int (&lo)[8], float& vmax, float& vmin, float& nanp,
-                                           float clampv = -INFINITY) {
+                                           float clampv EWK_PASS_PARAM) {
+    EWK_TS(fp0);
     EWK_SETPRIO(1);
     // lane group f = lane>>4 holds frames fr = 4 g + f (g < kNF) of this pass; the
     // kNF frames of a lane are independent instruction streams (ILP for the wave).
@@ -520,6 +527,7 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
         }
     }
     lds_order();
+    EWK_TS(fp1);
     // next pass's samples: issued before the mel stage (registers are free there),
     // stored to the staging area at the end of the pass
     float pf[kStageLoads];
@@ -535,6 +543,7 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
             }
         }
     }
+    EWK_TS(fp2);
     EWK_SETPRIO(1);
     // ---- transpose through LDS (real, then imaginary half): lane k1 <- A_{n2}[k1].
     // Row r (16 floats) keeps column n in 4-float chunk (n>>2) ^ ((r>>2)&3): the
@@ -570,10 +579,12 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
             lds_order();
         }
     }
+    EWK_TS(fp3);
     EWK_SETPRIO(0);
     // ---- DFT16 over n2: Z[j + 16*k2] = b[dperm(k2)]
 #pragma unroll
     for (int g = 0; g < kNF; ++g) dft16_perm(b[g]);
+    EWK_TS(fp4);
     // ---- untangle + power, two conjugate bins per step, no cross-lane traffic.  For
     // k = c0 + 16 it the partner Zp = Z[256 - k] sits in this lane's other column; with
     // A = Z[k] + conj(Zp), B = Z[k] - conj(Zp), C = i W512^k B:
@@ -652,6 +663,7 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
         if (jp < 7) scf[265 + jp] = 0.0f;
     }
     lds_order();
+    EWK_TS(fp5);
     EWK_SETPRIO(1);
     if (next_t0 >= 0) stage_load(v, next_t0 * HOP - NFFT / 2, lane, pf);
     // ---- mel + log: lane j computes bands m = j + 16*i of its frames (weights shared).
@@ -704,6 +716,7 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     }
     EWK_SETPRIO(0);
     lds_order();
+    EWK_TS(fp6);
     // Rows of frames past T keep their (finite: silence gives -100 dB) values: the DCT
     // columns are independent and the statistics skip those frames, so only the frame's
     // max/min needs the validity test, once per frame.  The eight bands of a lane form
@@ -729,6 +742,13 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
     lds_order();
     if (next_t0 >= 0) stage_store(scr, lane, pf);
     lds_order();
+#ifdef EWK_TIMING
+    EWK_TS(fp7);
+    if (pdbg) {
+        pdbg[12] += fp1 - fp0; pdbg[13] += fp2 - fp1; pdbg[14] += fp3 - fp2; pdbg[15] += fp4 - fp3;
+        pdbg[16] += fp5 - fp4; pdbg[17] += fp6 - fp5; pdbg[18] += fp7 - fp6; pdbg[19] += 1;
+    }
+#endif
 }
 
 // DCT of one 16-frame log-mel tile on the matrix cores: C[32 x 16] = D[32 x 128] X[128 x 16]
@@ -953,7 +973,7 @@ __device__ __forceinline__ void tile_passes(const SegSrc<RING>& v, int tile_i, i
         if ((mask >> p) & 1) {
             const int rest = mask >> (p + 1);   // the next selected pass of this tile is prefetched
             frame_pass(v, (p0 + p) * kFPP, T, p * kFPP, rest ? (p0 + p + 1 + __builtin_ctz(rest)) * kFPP : -1,
-                       smem, scr, tile, lane, lo, mx, mn, nanp, clampv);
+                       smem, scr, tile, lane, lo, mx, mn, nanp, clampv EWK_PASS_ARG(nullptr));
         } else {   // frames past T, or a pass left out: zero rows (their columns are not used)
             zero_rows(tile, p * kFPP, lane);
         }
@@ -1147,7 +1167,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
                                                                       : (next_tile >= 0 ? next_tile * 16 : -1);
             float tp = INFINITY;
             if (pass < npass)
-                frame_pass(v, pass * kFPP, T, p * kFPP, nxt, smem, scr, tile, lane, lo, vmax, tp, nanp, run);
+                frame_pass(v, pass * kFPP, T, p * kFPP, nxt, smem, scr, tile, lane, lo, vmax, tp, nanp, run EWK_PASS_ARG(dbg));
             else   // rows of frames past T: zero (ignored by the statistics)
                 zero_rows(tile, p * kFPP, lane);
             const float tpw = wave_min(tp);   // this pass's minimum (its record below)
@@ -1717,7 +1737,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
         return;
     }
 #ifdef EWK_TIMING
-    uint64_t dbg[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t dbg[kDbgN] = {};
 #endif
     const WorkCtx wc = {&a, base, count, true};
     WorkAhead nx;
@@ -1765,7 +1785,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
 #ifdef EWK_TIMING
     dbg[8] += 1;
     if (lane == 0)
-        for (int k = 0; k < 12; ++k) atomicAdd(&g_ewk_dbg[k], (unsigned long long)dbg[k]);
+        for (int k = 0; k < kDbgN; ++k) atomicAdd(&g_ewk_dbg[k], (unsigned long long)dbg[k]);
 #endif
     if (RING) ring_tick_end<RING>(a, smem, listed);
 }
@@ -1773,7 +1793,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
 #ifdef EWK_TIMING
 }  // namespace ewk
 extern "C" int ewk_debug_timing(unsigned long long* out) {   // read and reset (debug builds only)
-    unsigned long long z[12] = {};
+    unsigned long long z[kDbgN] = {};
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ewk::g_ewk_dbg), sizeof(z)) != hipSuccess) return -3;
     if (hipMemcpyToSymbol(HIP_SYMBOL(ewk::g_ewk_dbg), z, sizeof(z)) != hipSuccess) return -3;
     return 0;

@@ -36,7 +36,7 @@ print(f"{lib:28s} L={fixed or 'ragged'} {ms:8.3f} ms  {frames/ms/1e6:7.3f} Gfram
 import ctypes
 lib = ctypes.CDLL(os.environ.get("EWK_LIB") or os.path.join(ROOT, "easywakeword_amd", "libewk.so"))
 if hasattr(lib, "ewk_debug_timing"):   # -DEWK_TIMING builds (easywakeword_amd/libewk_timing.so)
-    buf = (ctypes.c_ulonglong * 12)()
+    buf = (ctypes.c_ulonglong * 20)()
     lib.ewk_debug_timing(buf)      # reset
     e.profile(False)
     step(); torch.cuda.synchronize()
@@ -49,3 +49,8 @@ if hasattr(lib, "ewk_debug_timing"):   # -DEWK_TIMING builds (easywakeword_amd/l
           ", ".join(f"{n}={buf[i] / segs:,.0f} ({100.0 * buf[i] / max(1, tot):.1f}%)" for i, n in enumerate(names)) +
           f"; recomputed tiles/segment={(buf[10] & 0xffff) / segs:.3f} passes/segment={buf[11] / segs:.3f} "
           f"parked fixes/segment={(buf[10] >> 16) / segs:.3f}")
+    if buf[19]:   # frame-pass sub-phases (first-pass passes only)
+        sub = ["window+DFT16a", "twiddle", "transposes", "DFT16b", "untangle+power", "mel+log", "tile write+stage"]
+        print(f"  per frame pass ({buf[19] / waves:,.0f} per wave): " +
+              ", ".join(f"{n}={buf[12 + i] / buf[19]:,.0f}" for i, n in enumerate(sub)) +
+              f"; total {sum(buf[12 + i] for i in range(7)) / buf[19]:,.0f} cycles")
