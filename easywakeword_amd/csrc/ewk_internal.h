@@ -22,7 +22,10 @@ constexpr int SCR_FRAME = 272;       // per-frame FFT scratch floats (16 rows x 
 // instruction streams per lane; the untangle pairs conjugate bins inside a lane), eight
 // waves per workgroup, one workgroup per CU (2 waves per SIMD at 256 VGPRs).
 constexpr int kNF = 2;
-constexpr int WAVES = 8;
+#ifndef EWK_WAVES
+#define EWK_WAVES 8
+#endif
+constexpr int WAVES = EWK_WAVES;   // waves per scorer workgroup (one workgroup per CU)
 // start (floats) of frame fr's FFT scratch / power spectrum in a scorer wave's LDS scratch:
 // the two frames a 16-lane group untangles side by side (fr, fr + 4) land 8 banks apart
 __host__ __device__ constexpr int scr_frame_off(int fr) { return fr * SCR_FRAME + 8 * (fr >> 2); }
