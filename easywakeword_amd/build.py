@@ -65,5 +65,20 @@ def build(force: bool = False, verbose: bool = False, out: str = None, defines=(
     return lib
 
 
+ROOT = os.path.dirname(HERE)
+C_HOST_SRC = os.path.join(ROOT, "examples", "c_positives_rccl.cpp")
+C_HOST_BIN = os.path.join(ROOT, "examples", "c_positives_rccl")
+
+
+def build_c_host(verbose: bool = False) -> str:
+    """The C-host example (examples/c_positives_rccl.cpp): libewk.so + RCCL, no Python."""
+    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"),
+           C_HOST_SRC, "-L", HERE, "-lewk", "-lrccl", "-Wl,-rpath,$ORIGIN/../easywakeword_amd", "-o", C_HOST_BIN]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    return C_HOST_BIN
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))

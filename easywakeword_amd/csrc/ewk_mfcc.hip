@@ -69,7 +69,9 @@
 #define EWK_PASS_PARAM
 #define EWK_PASS_ARG(x)
 #endif
+#ifdef EWK_TIMING
 constexpr int kDbgN = 20;
+#endif
 
 namespace ewk {
 
