@@ -48,6 +48,13 @@
 #include "ewk_internal.h"
 
 // s_setprio 1 over the frame-pass LDS phases (window, transposes, mel): -0.4 %
+// round-3 VALU cuts (A/B switches while measured): -DEWK_NO_MIX / -DEWK_NO_UNTAN
+#ifndef EWK_NO_MIX
+#define EWK_XP_MIX 1
+#endif
+#ifndef EWK_NO_UNTAN
+#define EWK_XP_UNTAN 1
+#endif
 #define EWK_SETPRIO(v) __builtin_amdgcn_s_setprio(v)
 
 // Per-wave phase timing of the linear-batch scorer (debug builds with -DEWK_TIMING only:
@@ -124,6 +131,7 @@ constexpr int L_DCT = L_BLO + NMEL * 4;
 // [q][hi/lo][lane] 16-B chunks; row tile 1 (coefficients 16..19): [q][hi/lo][l >> 4][l & 3]
 // for the lanes with (l & 15) < 4, every other lane reads the block's zero chunk.
 constexpr float kDctScale = 1024.0f;
+constexpr float kTopDbUnits = 80.0f;   // top_db, in the tile's dB units
 constexpr int DCT_RT1 = 4 * 2 * 64 * 16;                  // row tile 1: [q][hi/lo] blocks of 17 chunks
 constexpr int DCT_RT1_STRIDE = 17 * 16;                   // 16 data chunks [l >> 4][l & 3] + a zero chunk
 constexpr int DCT_BYTES = DCT_RT1 + 8 * DCT_RT1_STRIDE;
@@ -270,6 +278,25 @@ __device__ __forceinline__ uint32_t pk_f16(float a, float b) {   // v_cvt_pk_f16
 __device__ __forceinline__ float f16_lo(uint32_t p) { return (float)__builtin_bit_cast(halfx2, p).x; }
 __device__ __forceinline__ float f16_hi(uint32_t p) { return (float)__builtin_bit_cast(halfx2, p).y; }
 // eight log-mel values -> their hi chunk and lo chunk (16 B each)
+#ifdef EWK_XP_MIX
+// hi pair = v_cvt_pkrtz_f16_f32 (round toward zero = the 11-bit truncation over the dB
+// range), lo = f16(x - float(hi)) by v_fma_mixlo/mixhi_f16 (the subtraction in f32, exact;
+// one rounding to f16): 3 VALU per pair instead of 6.
+__device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& l) {
+    h = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
+    uint32_t r;
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %0, %3, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "=&v"(r) : "v"(a), "v"(h), "v"(b));
+    l = r;
+}
+__device__ __forceinline__ void split8(const float (&x)[8], uint4& hi, uint4& lo) {
+    split2(x[0], x[1], hi.x, lo.x);
+    split2(x[2], x[3], hi.y, lo.y);
+    split2(x[4], x[5], hi.z, lo.z);
+    split2(x[6], x[7], hi.w, lo.w);
+}
+#else
 __device__ __forceinline__ void split8(const float (&x)[8], uint4& hi, uint4& lo) {
     float h[8], l[8];
 #pragma unroll
@@ -277,6 +304,7 @@ __device__ __forceinline__ void split8(const float (&x)[8], uint4& hi, uint4& lo
     hi = make_uint4(pk_f16(h[0], h[1]), pk_f16(h[2], h[3]), pk_f16(h[4], h[5]), pk_f16(h[6], h[7]));
     lo = make_uint4(pk_f16(l[0], l[1]), pk_f16(l[2], l[3]), pk_f16(l[4], l[5]), pk_f16(l[6], l[7]));
 }
+#endif
 // Byte offset of k-chunk c of frame row r in the log-mel tile: the row's hi chunks fill its
 // first 256 B and the lo chunks the next 256 B, chunk c at slot c ^ r, so the 16 rows of a
 // DCT operand read (one chunk per row) and the 16 chunks of a row write both cover all
@@ -638,10 +666,17 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
                 }
                 const float ar = uu.x + vv.x, ai = uu.y - vv.y;
                 const float br = uu.x - vv.x, bi = uu.y + vv.y;
+#ifdef EWK_XP_UNTAN
+                // w = (c, t = s / c): C = c (t br - bi, t bi + br), its scale in the output FMAs
+                const float er = fmaf(w.y, br, -bi), ei = fmaf(w.y, bi, br);
+                const float yr = fmaf(-w.x, er, ar), yi = fmaf(-w.x, ei, ai);
+                const float xr = fmaf(w.x, er, ar), xi = fmaf(w.x, ei, ai);
+#else
                 const float cr = w.y * br - w.x * bi;
                 const float ci = w.y * bi + w.x * br;
                 const float yr = ar - cr, yi = ai - ci;
                 const float xr = ar + cr, xi = ai + ci;
+#endif
                 py[u] = yr * yr + yi * yi;
                 px[u] = xr * xr + xi * xi;
             }
@@ -1182,7 +1217,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
         if (last && wc.ahead) work_order<RING>(wc, nx);
         // max(max(x, run), final) = max(x, final): a tile stored clamped at the running max
         // (this tile's own values included) is exact unless a later tile raises the max
-        const float run2 = rec ? wave_max(vmax) - 80.0f : -INFINITY;
+        const float run2 = rec ? wave_max(vmax) - kTopDbUnits : -INFINITY;
         if (run2 > run && tmw < run2) {   // this tile raised the max over some of its own values
             uint4 h[4], l[4];
             clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
@@ -1212,7 +1247,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     if (wc.ahead) work_describe<RING>(wc, nx);
     // wave-wide log-mel max
     vmax = wave_max(vmax);
-    const float theta = vmax - 80.0f;
+    const float theta = vmax - kTopDbUnits;
     if (vmin < theta) {
         lds_order();
         for (int cur = 0; cur < ntile; ++cur) {
@@ -1278,7 +1313,7 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
         const float tmw = wave_min(tmin);
         vmin = fminf(vmin, tmw);
         if (last) { last_min = tmw; break; }
-        const float run2 = rec ? wave_max(vmax) - 80.0f : -INFINITY;
+        const float run2 = rec ? wave_max(vmax) - kTopDbUnits : -INFINITY;
         if (run2 > run && tmw < run2) {   // self-clamp (segment_stats)
             uint4 h[4], l[4];
             clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
@@ -1304,7 +1339,7 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
     __syncthreads();
 #pragma unroll
     for (int w = 0; w < WAVES; ++w) { vmax = fmaxf(vmax, wg_mm[2 * w]); vmin = fminf(vmin, wg_mm[2 * w + 1]); }
-    const float theta = vmax - 80.0f;
+    const float theta = vmax - kTopDbUnits;
     if (nloc > 0) {
         const int tile_l = wave + WAVES * (nloc - 1);
         if (last_min < theta) {   // the last tile, still in LDS: clamp at the final threshold
@@ -1642,7 +1677,12 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
         for (int i = threadIdx.x; i < 8 * 17; i += blockDim.x) {
             const int jp = i / 17, it = i % 17;
             const int k = jp ? jp + 16 * (it < 16 ? it : 15) : (it <= 8 ? 16 * it : 8 + 16 * (it - 9));
+#ifdef EWK_XP_UNTAN
+            const float2 cs = tab->tw2[k];   // (c, t): c = cos is never 0 in float (k = 128: 6.1e-17)
+            st2[jp * TP + it] = make_float2(cs.x, cs.y / cs.x);
+#else
             st2[jp * TP + it] = tab->tw2[k];
+#endif
         }
         int* sb = reinterpret_cast<int*>(smem + L_BLO);
         for (int i = threadIdx.x; i < NMEL; i += blockDim.x) sb[i] = tab->band_lo[i];
