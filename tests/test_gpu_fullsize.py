@@ -110,4 +110,37 @@ def test_config3_streams_full_size_sampled_vs_oracle(env):
             assert bool(m["match"]) == (s >= 75.0)
             n_checked += 1
     assert n_checked >= 100                             # 138 level-2 calls on these 8 streams
+
+    # Every part of the grid: 4,096 events drawn over all streams and ticks (pushes of 32
+    # ticks score a few thousand segments per launch: teams of 2 waves in rounds, 4 or 8 on
+    # lighter launches) re-scored by the linear batch scorer from the stream audio.  The
+    # segment is the `length` samples from tick * 1600 - n_request, where n_request =
+    # (tick * 1600 - ring_start) mod ring (checked against the oracle's cut on the samples).
+    ring = 160000
+    lp = period * 1600
+
+    def cut(row, m):
+        n_req = (int(m["tick"]) * 1600 - int(m["ring_start"])) % ring
+        s0 = int(m["tick"]) * 1600 - n_req
+        return row[np.arange(s0, s0 + int(m["length"])) % lp]
+
+    for row, sid in zip(host, sample):
+        mine = ev[(ev["stream"] == sid) & ((ev["flags"] & 1) == 0)]
+        ref = [e for e in run_stream(np.tile(row, reps)[: ticks * 1600], GateConfig()).events if not e.skipped]
+        for m, e in zip(mine[np.argsort(mine["tick"], kind="stable")], ref):
+            np.testing.assert_array_equal(cut(row, m), e.audio.astype(np.float32))
+    scored = ev[(ev["flags"] & 1) == 0]
+    pick = np.random.Generator(np.random.PCG64(7)).choice(len(scored), size=min(4096, len(scored)), replace=False)
+    pick = scored[np.sort(pick)]
+    rows = pcm[torch.from_numpy(pick["stream"].astype(np.int64)).to(pcm.device)].cpu().numpy()
+    segs = [cut(r, m) for r, m in zip(rows, pick)]
+    eng = ewa.Engine()
+    eng.template_from_pcm(word)
+    _, _, sc, mt = eng.score(segs, candidate_dtype="float64")
+    d = np.abs(sc - pick["score"])
+    fin = np.isfinite(sc)
+    assert np.array_equal(fin, np.isfinite(pick["score"]))
+    assert float(d[fin].max()) <= 2 * SCORE_TOL, (float(d[fin].max()), pick[np.argmax(np.where(fin, d, 0))])
+    np.testing.assert_array_equal(mt.astype(bool), pick["match"].astype(bool))
+    eng.close()
     se.close()
