@@ -48,13 +48,6 @@
 #include "ewk_internal.h"
 
 // s_setprio 1 over the frame-pass LDS phases (window, transposes, mel): -0.4 %
-// round-3 VALU cuts (A/B switches while measured): -DEWK_NO_MIX / -DEWK_NO_UNTAN
-#ifndef EWK_NO_MIX
-#define EWK_XP_MIX 1
-#endif
-#ifndef EWK_NO_UNTAN
-#define EWK_XP_UNTAN 1
-#endif
 #define EWK_SETPRIO(v) __builtin_amdgcn_s_setprio(v)
 
 // Per-wave phase timing of the linear-batch scorer (debug builds with -DEWK_TIMING only:
@@ -278,7 +271,6 @@ __device__ __forceinline__ uint32_t pk_f16(float a, float b) {   // v_cvt_pk_f16
 __device__ __forceinline__ float f16_lo(uint32_t p) { return (float)__builtin_bit_cast(halfx2, p).x; }
 __device__ __forceinline__ float f16_hi(uint32_t p) { return (float)__builtin_bit_cast(halfx2, p).y; }
 // eight log-mel values -> their hi chunk and lo chunk (16 B each)
-#ifdef EWK_XP_MIX
 // hi pair = v_cvt_pkrtz_f16_f32 (round toward zero = the 11-bit truncation over the dB
 // range), lo = f16(x - float(hi)) by v_fma_mixlo/mixhi_f16 (the subtraction in f32, exact;
 // one rounding to f16): 3 VALU per pair instead of 6.
@@ -296,15 +288,6 @@ __device__ __forceinline__ void split8(const float (&x)[8], uint4& hi, uint4& lo
     split2(x[4], x[5], hi.z, lo.z);
     split2(x[6], x[7], hi.w, lo.w);
 }
-#else
-__device__ __forceinline__ void split8(const float (&x)[8], uint4& hi, uint4& lo) {
-    float h[8], l[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { h[i] = f16_trunc(x[i]); l[i] = x[i] - h[i]; }
-    hi = make_uint4(pk_f16(h[0], h[1]), pk_f16(h[2], h[3]), pk_f16(h[4], h[5]), pk_f16(h[6], h[7]));
-    lo = make_uint4(pk_f16(l[0], l[1]), pk_f16(l[2], l[3]), pk_f16(l[4], l[5]), pk_f16(l[6], l[7]));
-}
-#endif
 // Byte offset of k-chunk c of frame row r in the log-mel tile: the row's hi chunks fill its
 // first 256 B and the lo chunks the next 256 B, chunk c at slot c ^ r, so the 16 rows of a
 // DCT operand read (one chunk per row) and the 16 chunks of a row write both cover all
@@ -651,7 +634,7 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
             for (int u = 0; u < 2; ++u) {
                 const int it = it0 + u;
                 if (it >= 17) break;
-                const float2 w = tw[it];   // (cos, sin)(2 pi k / 512)
+                const float2 w = tw[it];   // (cos, tan)(2 pi k / 512)
                 const float2 ug = b[0][dperm(it < 16 ? it : 15)];
                 const float2 vg = b[1][dperm(it < 16 ? 15 - it : 0)];
                 float2 uu, vv;
@@ -666,17 +649,10 @@ __device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T,
                 }
                 const float ar = uu.x + vv.x, ai = uu.y - vv.y;
                 const float br = uu.x - vv.x, bi = uu.y + vv.y;
-#ifdef EWK_XP_UNTAN
                 // w = (c, t = s / c): C = c (t br - bi, t bi + br), its scale in the output FMAs
                 const float er = fmaf(w.y, br, -bi), ei = fmaf(w.y, bi, br);
                 const float yr = fmaf(-w.x, er, ar), yi = fmaf(-w.x, ei, ai);
                 const float xr = fmaf(w.x, er, ar), xi = fmaf(w.x, ei, ai);
-#else
-                const float cr = w.y * br - w.x * bi;
-                const float ci = w.y * bi + w.x * br;
-                const float yr = ar - cr, yi = ai - ci;
-                const float xr = ar + cr, xi = ai + ci;
-#endif
                 py[u] = yr * yr + yi * yi;
                 px[u] = xr * xr + xi * xi;
             }
@@ -1673,16 +1649,12 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
             sw2[j * TP + n] = make_float2(tab->win2[i].x * kWinScale, tab->win2[i].y * kWinScale);
             if (n > 0) st1[j * TP + n - 1] = tab->tw1[i];
         }
-        // [j'][it] = tw2[k] for the bin k that lane class j' untangles at step it
+        // [j'][it] = (cos, tan) of tw2[k] for the bin k that lane class j' untangles at step it
         for (int i = threadIdx.x; i < 8 * 17; i += blockDim.x) {
             const int jp = i / 17, it = i % 17;
             const int k = jp ? jp + 16 * (it < 16 ? it : 15) : (it <= 8 ? 16 * it : 8 + 16 * (it - 9));
-#ifdef EWK_XP_UNTAN
             const float2 cs = tab->tw2[k];   // (c, t): c = cos is never 0 in float (k = 128: 6.1e-17)
             st2[jp * TP + it] = make_float2(cs.x, cs.y / cs.x);
-#else
-            st2[jp * TP + it] = tab->tw2[k];
-#endif
         }
         int* sb = reinterpret_cast<int*>(smem + L_BLO);
         for (int i = threadIdx.x; i < NMEL; i += blockDim.x) sb[i] = tab->band_lo[i];
