@@ -176,3 +176,35 @@ def matcher_cases():
         cases.append((f"word_in_hp_{g:g}", (word * np.float32(g) + np.diff(rng.standard_normal(n + 1)) * 0.08)
                       .astype(np.float32)))
     return [(n, np.ascontiguousarray(x, dtype=np.float32)) for n, x in cases]
+
+
+def fuzz_segments(seed: int, n: int, word: np.ndarray) -> list:
+    """The top_db fuzz recipe (tests/test_gpu_scorer.py): lengths 1-60000, a noise floor of
+    1e-7..1e-2, 0-4 bursts (the word, a tone or white noise, 0-100 dB above the floor) at
+    random places, a 3000-sample digital-silence stretch every 7th segment and two identical
+    2560-sample tiles (a scout tie) every 11th."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    segs = []
+    for k in range(n):
+        L = int(rng.integers(1, 60001))
+        x = (rng.normal(0, 1, L) * 10 ** rng.uniform(-7, -2)).astype(np.float32)
+        for _ in range(int(rng.integers(0, 5))):
+            m = int(rng.integers(200, 12000))
+            s0 = int(rng.integers(0, max(1, L - m)))
+            amp = np.float32(10 ** rng.uniform(-5, 0))
+            kind = int(rng.integers(0, 3))
+            if kind == 0:
+                src = word[:m] if m <= len(word) else np.resize(word, m)
+            elif kind == 1:
+                src = np.sin(2 * np.pi * rng.uniform(100, 7000) * np.arange(m) / 16000).astype(np.float32)
+            else:
+                src = rng.normal(0, 1, m).astype(np.float32)
+            c = min(m, L - s0)
+            x[s0:s0 + c] += amp * src[:c]
+        if k % 7 == 0 and L > 4000:       # digital silence stretch
+            a = int(rng.integers(0, L - 3000))
+            x[a:a + 3000] = 0.0
+        if k % 11 == 0 and L > 5120:      # two identical tiles: a tie in the scout ranking
+            x[2560:5120] = x[0:2560]
+        segs.append(x)
+    return segs

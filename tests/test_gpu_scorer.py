@@ -242,39 +242,10 @@ def test_top_db_past_the_tile_record(engine):
         assert bool(match[i]) == (ref >= 75.0)
 
 
-def test_top_db_order_fuzz(engine):
-    """Randomised segments for the loudest-first order, the self-clamp and the recompute of
-    tiles the final top_db threshold bites: 0-4 bursts of random level (0-100 dB above a
-    random noise floor) at random places, stretches of digital silence (the -100 dB amin
-    floor), equal-energy tiles (ties in the scout ranking), lengths 1-60000 samples.  Every
-    score must equal the oracle's within 1e-4 with the same decision."""
+def _fuzz_vs_oracle(engine, seed, n):
     engine.template_from_pcm(synth.load_word())
     tm, ts = engine.get_template()
-    rng = np.random.Generator(np.random.PCG64(2024))
-    word = synth.load_word()
-    segs = []
-    for k in range(120):
-        L = int(rng.integers(1, 60001))
-        x = (rng.normal(0, 1, L) * 10 ** rng.uniform(-7, -2)).astype(np.float32)
-        for _ in range(int(rng.integers(0, 5))):
-            n = int(rng.integers(200, 12000))
-            s0 = int(rng.integers(0, max(1, L - n)))
-            amp = np.float32(10 ** rng.uniform(-5, 0))
-            kind = int(rng.integers(0, 3))
-            if kind == 0:
-                src = word[:n] if n <= len(word) else np.resize(word, n)
-            elif kind == 1:
-                src = np.sin(2 * np.pi * rng.uniform(100, 7000) * np.arange(n) / 16000).astype(np.float32)
-            else:
-                src = rng.normal(0, 1, n).astype(np.float32)
-            m = min(n, L - s0)
-            x[s0:s0 + m] += amp * src[:m]
-        if k % 7 == 0 and L > 4000:       # digital silence stretch
-            a = int(rng.integers(0, L - 3000))
-            x[a:a + 3000] = 0.0
-        if k % 11 == 0 and L > 5120:      # two identical tiles: a tie in the scout ranking
-            x[2560:5120] = x[0:2560]
-        segs.append(x)
+    segs = synth.fuzz_segments(seed, n, synth.load_word())
     _, _, score, match = engine.score(segs, candidate_dtype="float64")
     n_const = 0
     for i, x in enumerate(segs):
@@ -288,9 +259,28 @@ def test_top_db_order_fuzz(engine):
             continue
         cm, cs = mfcc_ref.extract_mfcc(x.astype(np.float64))
         ref = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
-        assert score_close(score[i], ref, SCORE_TOL), (i, len(x), score[i], ref)
-        assert bool(match[i]) == (ref >= 75.0), (i, score[i], ref)
+        assert score_close(score[i], ref, SCORE_TOL), (seed, i, len(x), score[i], ref)
+        assert bool(match[i]) == (ref >= 75.0), (seed, i, score[i], ref)
+    return n_const
+
+
+def test_top_db_order_fuzz(engine):
+    """Randomised segments for the loudest-first order, the self-clamp and the recompute of
+    tiles the final top_db threshold bites: 0-4 bursts of random level (0-100 dB above a
+    random noise floor) at random places, stretches of digital silence (the -100 dB amin
+    floor), equal-energy tiles (ties in the scout ranking), lengths 1-60000 samples.  Every
+    score must equal the oracle's within 1e-4 with the same decision."""
+    n_const = _fuzz_vs_oracle(engine, 2024, 120)
     assert 0 < n_const < 10
+
+
+@pytest.mark.parametrize("seed", [3, 5, 7, 12])
+def test_fuzz_stationary_segments(engine, seed):
+    """More seeds of the same recipe, the ones whose steady-noise segments (MFCC std vectors
+    of norm 2-8, no speech contrast) missed 1e-4 by up to 2.9e-4 in float32 before such
+    segments (|std| < 20; the bench's ragged batch has >= 24.8, the streaming recipe's
+    events >= 32.5) went to the fp64 re-score (scripts/fuzz_err.py, scripts/std_norm_dist.py)."""
+    _fuzz_vs_oracle(engine, seed, 200)
 
 
 def test_non_finite_samples_do_not_disturb_the_batch(engine):
