@@ -1,5 +1,6 @@
-"""|std| (the MFCC std vector's norm) over the bench's batch and over streaming events: how many
-segments a |std| < X fp64 re-score criterion would send to k_score_f64 (DESIGN.md numerics)."""
+"""|std| and |mean| (the MFCC std / mean vectors' norms) over the bench's batch and over
+streaming events: how many segments a |std| < X or |mean| < Y fp64 re-score criterion would
+send to k_score_f64 (DESIGN.md numerics)."""
 import os, sys
 import numpy as np
 ROOT = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -12,7 +13,13 @@ word = bench.load_word()
 TH = (2, 4, 8, 12, 16, 20)
 
 
-def report(name, s):
+def report(name, s, m=None):
+    if m is not None:
+        mn = np.linalg.norm(m, axis=1)
+        mn = mn[np.isfinite(mn)]
+        qm = np.quantile(mn, [0, 0.001, 0.01, 0.1, 0.5, 1.0])
+        print(f"{name}: |mean| min {qm[0]:.1f} p0.1 {qm[1]:.1f} p1 {qm[2]:.1f} p10 {qm[3]:.1f} median {qm[4]:.1f} max {qm[5]:.1f}; "
+              + ", ".join(f"<{t}: {int(np.sum(mn < t))}" for t in (100, 200, 300, 400, 500)))
     n = np.linalg.norm(s, axis=1)
     n = n[np.isfinite(n)]
     q = np.quantile(n, [0, 0.001, 0.01, 0.1, 0.5])
@@ -26,7 +33,7 @@ e = ewa.Engine()
 e.template_from_pcm(word)
 host = pcm.cpu().numpy()
 m, s, sc, mt = e.score_packed(host, offsets, lengths, True, False)
-report("bench batch (configs[1])", s)
+report("bench batch (configs[1])", s, m)
 del pcm
 n_streams, ticks = 8192, 400
 period, spcm = bench.make_streams(torch, dev, n_streams, 1234, word)
@@ -50,4 +57,15 @@ for r, ev1 in zip(rows, pick):
     s0 = int(ev1["tick"]) * 1600 - n_req
     segs.append(r[np.arange(s0, s0 + int(ev1["length"])) % lp])
 m2, s2, sc2, mt2 = e.score(segs, candidate_dtype="float64")
-report("streaming events (configs[2] recipe)", s2)
+report("streaming events (configs[2] recipe)", s2, m2)
+# fp32 score vs the device fp64 path on the streaming segments, by |mean| bucket
+m64, s64, sc64 = e.score_f64(segs)
+mn = np.linalg.norm(m2, axis=1)
+d = np.abs(sc2 - sc64)
+ok = np.isfinite(sc2) & np.isfinite(sc64)
+for lo_, hi_ in ((0, 50), (50, 100), (100, 200), (200, 400), (400, 1e9)):
+    sel = ok & (mn >= lo_) & (mn < hi_)
+    if sel.any():
+        print(f"streaming |mean| in [{lo_}, {hi_}): {int(sel.sum())} scored, |dscore| vs fp64 max {d[sel].max():.3e} "
+              f"median {np.median(d[sel]):.3e}")
+print("NaN agreement:", bool(np.array_equal(np.isnan(sc2), np.isnan(sc64))))
