@@ -140,6 +140,8 @@ constexpr int W_BYTES = W_SPEC + (kSpecOrder + kSpecTiles) * 4;
 constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
 constexpr int LDS_BYTES = L_WG + 16 + 8 * WAVES;
 constexpr int kRescoreFrames = 16;
+constexpr double kTinyMean = 64.0;  // |mean vector| below which linear batches re-score in fp64
+                                    // (loud audio, c0 cancelling: DESIGN.md numerics, "Known gap")
 constexpr double kTinyStd = 20.0;   // |std vector| below which the fp64 path decides (bench batch >= 24.8,
                                     // streaming events >= 32.5: scripts/std_norm_dist.py)
 static_assert(LDS_BYTES <= 160 * 1024, "the workgroup must fit a CU's LDS");
@@ -1490,17 +1492,19 @@ __device__ __forceinline__ double score_f32_finish(float uu_m, float uu_s, float
 template <int RING>
 __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, float csf, float tmf, float tsf,
                                                int lane, int seg, int len, bool& listed) {
-    double score, std2;
+    double score, std2, mean2;
     if (a.cand_f32) {   // float32 candidates: float products, float-rounded dots (sdot)
         const float uv_m = (float)wave_sum_d((double)(tmf * cmf)), vv_m = (float)wave_sum_d((double)(cmf * cmf));
         const float uv_s = (float)wave_sum_d((double)(tsf * csf)), vv_s = (float)wave_sum_d((double)(csf * csf));
         score = score_f32_finish(a.uu_m32, a.uu_s32, uv_m, vv_m, uv_s, vv_s);
         std2 = vv_s;
+        mean2 = vv_m;
     } else {
         const double uv_m = wave_sum_d((double)tmf * (double)cmf), vv_m = wave_sum_d((double)cmf * (double)cmf);
         const double uv_s = wave_sum_d((double)tsf * (double)csf), vv_s = wave_sum_d((double)csf * (double)csf);
         score = score_f64_finish((double)a.uu_m32, (double)a.uu_s32, uv_m, vv_m, uv_s, vv_s);
         std2 = vv_s;
+        mean2 = vv_m;
     }
     if (lane == 0) {
         const int match = score >= a.threshold;
@@ -1513,7 +1517,10 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, fl
         // |std| = 8).  An exactly constant segment keeps its NaN (zero std; the reference's own
         // value there is a rounding artefact).
         const bool near = fabs(score - a.threshold) < a.rescore_margin || (1 + len / HOP) <= kRescoreFrames ||
-                          (std2 > 0.0 && std2 < kTinyStd * kTinyStd);
+                          (std2 > 0.0 && std2 < kTinyStd * kTinyStd) ||
+                          // linear batches only: a ring tick re-scores its list in one workgroup,
+                          // serially (4 % of a burst's events would cost ~4 ms per tick)
+                          (!RING && mean2 < kTinyMean * kTinyMean);
         if (RING) {
             a.events[seg].score = score;
             a.events[seg].match = match;

