@@ -207,7 +207,25 @@ class PositiveCollector:
         take = pos[:self.audio_cap]
         if len(pos) > len(take):
             self.pending.append(pos[len(take):])
-        self.captured.insert(0, (take, list(self.audio_fn(take))))   # polls arrive in tick order
+        try:
+            pcm = list(self.audio_fn(take))
+        except ValueError:
+            # some events' samples were overwritten in their ring before this poll (a poll
+            # more than (ring - request) / block ticks behind the cut: multi-tick pushes,
+            # compact rings): those go on as records without PCM, the rest keep theirs
+            keep, pcm, lost = [], [], []
+            for i in range(len(take)):
+                try:
+                    pcm.extend(self.audio_fn(take[i:i + 1]))
+                    keep.append(i)
+                except ValueError:
+                    lost.append(i)
+            if lost:
+                self.pending.append(take[lost])
+            take = take[keep]
+            if not len(take):
+                return
+        self.captured.insert(0, (take, pcm))   # polls arrive in tick order
         kept = 0
         for i, (ev, pcm) in enumerate(self.captured):   # keep the newest audio_cap captures
             room = self.audio_cap - kept
