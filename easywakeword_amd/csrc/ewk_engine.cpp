@@ -80,16 +80,18 @@ struct ewk_engine {
     float uu_m32 = 0.f, uu_s32 = 0.f;   // numpy float32 dot of the template with itself
     bool has_tmpl = false;
 
-    // rescoring
-    DevBuf<int32_t> rescore_buf;    // [0] = count, [1..] list
-    int32_t* d_rescore = nullptr;   // == rescore_buf.p
-    int32_t* d_work = nullptr;      // scorer work counter
+    // fp64 re-score (ewk_rescore.h): slots of listed segments and the chunk part pool, shared
+    // by linear and ring launches (which never run concurrently: join_scoring)
+    DevBuf<RsSlot> rs_slots;        // zeroed: nclaim 0 = not published
+    DevBuf<RsPart> rs_parts;
+    int32_t rs_cap = 0;             // slots
+    int32_t rs_part_cap = 0;        // part records (a slot that finds the pool full runs serially)
+    // [0] linear work, [1] ring work, [4..5] event-count snapshots, [8..11] ring re-score
+    // counters (ScoreArgs::rs_ctl), [12..15] linear re-score counters
+    int32_t* d_work = nullptr;
     int32_t* d_compact = nullptr;   // ewk_compact_positives block counts / offsets
     int32_t compact_cap = 0;        // ... in blocks
     DevBuf<int32_t> order;          // linear batches: longest-first work order (k_lpt_order)
-    int32_t rescore_cap = 4096;
-    DevBuf<double> f64_scratch;
-    int f64_grid = 64;
 
     // host-API staging
     DevBuf<float> pcm;
@@ -216,19 +218,31 @@ static hipError_t join_scoring(ewk_engine* e, hipStream_t s) {
     return hipStreamWaitEvent(s, e->score_tail, 0);
 }
 
-// The re-score list holds at most one entry per segment of a launch.
+// The re-score list holds at most one slot per segment of a launch (slots must start zeroed).
 static hipError_t reserve_rescore(ewk_engine* e, int32_t n_seg) {
-    if (n_seg <= e->rescore_cap) return hipSuccess;
-    hipError_t err = hipStreamSynchronize(e->stream);
+    if (n_seg <= e->rs_cap) return hipSuccess;
+    hipError_t err = hipSuccess;
+    if (e->stream) err = hipStreamSynchronize(e->stream);
     if (err == hipSuccess && e->sstream) err = hipStreamSynchronize(e->sstream);
     if (err != hipSuccess) return err;
-    err = e->rescore_buf.reserve((size_t)n_seg + 1);
+    err = e->rs_slots.reserve((size_t)n_seg);
+    if (err == hipSuccess) err = hipMemset(e->rs_slots.p, 0, (size_t)n_seg * sizeof(RsSlot));
     if (err != hipSuccess) return err;
-    e->d_rescore = e->rescore_buf.p;
     err = e->order.reserve((size_t)n_seg + kLptScratch);
     if (err != hipSuccess) return err;
-    e->rescore_cap = n_seg;
+    e->rs_cap = n_seg;
     return hipSuccess;
+}
+
+// Part records for the chunks of the slots listed in one launch (8 frames each).
+static hipError_t reserve_parts(ewk_engine* e, int32_t n) {
+    if (n <= e->rs_part_cap) return hipSuccess;
+    hipError_t err = hipSuccess;
+    if (e->stream) err = hipStreamSynchronize(e->stream);
+    if (err == hipSuccess && e->sstream) err = hipStreamSynchronize(e->sstream);
+    if (err == hipSuccess) err = e->rs_parts.reserve((size_t)n);
+    if (err == hipSuccess) e->rs_part_cap = n;
+    return err;
 }
 
 extern "C" {
@@ -289,10 +303,10 @@ void ewk_destroy(ewk_engine* e) {
     (void)hipFree(e->d_tab);
     (void)hipFree(e->d_tab64);
     (void)hipFree(e->d_tmpl);
-    e->rescore_buf.release();
+    e->rs_slots.release();
+    e->rs_parts.release();
     (void)hipFree(e->d_work);
     (void)hipFree(e->d_compact);
-    e->f64_scratch.release();
     e->order.release();
     e->pcm.release();
     e->offsets.release();
@@ -415,17 +429,10 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
             return bail(err, "tables64");
     }
     if ((err = hipMalloc(&e->d_tmpl, 2 * NMFCC * sizeof(float))) != hipSuccess) return bail(err, "template");
-    if ((err = e->rescore_buf.reserve(1 + e->rescore_cap)) != hipSuccess) return bail(err, "rescore");
-    e->d_rescore = e->rescore_buf.p;
-    // [0] linear work counter, [1] ring work counter, [2] ring re-score count, [4..5] event-count snapshots
-    if ((err = hipMalloc(&e->d_work, 8 * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
-    if ((err = hipMemset(e->d_work, 0, 8 * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
-    // fp64 scratch: log-mel + mfcc rows for the longest ring segment
-    {
-        const int64_t tmax = 1 + e->sring_len / HOP;
-        const int64_t per = tmax * (NMEL + NMFCC);
-        if ((err = e->f64_scratch.reserve((size_t)per * e->f64_grid)) != hipSuccess) return bail(err, "f64 scratch");
-    }
+    if ((err = reserve_rescore(e, 4096)) != hipSuccess) return bail(err, "rescore slots");
+    if ((err = reserve_parts(e, 16384)) != hipSuccess) return bail(err, "rescore parts");
+    if ((err = hipMalloc(&e->d_work, 16 * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
+    if ((err = hipMemset(e->d_work, 0, 16 * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
     if (n_streams > 0) {
         const size_t ring_bytes = (size_t)n_streams * e->sring_len * e->ring_es;
         if ((err = hipMalloc(&e->d_ring, ring_bytes)) != hipSuccess) return bail(err, "ring");
@@ -451,6 +458,9 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
         }
         e->ev_cap = std::max(4096, 4 * n_streams);
         if ((err = reserve_rescore(e, e->ev_cap)) != hipSuccess) return bail(err, "rescore list");
+        // a tick lists ~4 % of its events (the configs[2] recipe), ~20 chunks each
+        if ((err = reserve_parts(e, std::min(262144, std::max(16384, e->ev_cap / 2)))) != hipSuccess)
+            return bail(err, "rescore parts");
         if ((err = hipMalloc(&e->d_events, 2 * (size_t)e->ev_cap * sizeof(ewk_event))) != hipSuccess)
             return bail(err, "events");
         if ((err = hipMalloc(&e->d_evc, 8 * sizeof(int32_t))) != hipSuccess) return bail(err, "event counters");
@@ -536,9 +546,12 @@ static ScoreArgs base_args(ewk_engine* e) {
     a.uu_s32 = e->uu_s32;
     a.threshold = e->cfg.similarity_threshold;
     a.rescore_margin = e->cfg.rescore_margin;
-    a.rescore_count = e->d_rescore;
-    a.rescore_list = e->d_rescore + 1;
-    a.rescore_cap = e->rescore_cap;
+    a.rs_ctl = e->d_work + 12;
+    a.rs_slots = e->has_tmpl ? e->rs_slots.p : nullptr;
+    a.rs_cap = e->rs_cap;
+    a.rs_parts = e->rs_parts.p;
+    a.rs_part_cap = e->rs_part_cap;
+    a.tab64 = e->d_tab64;
     a.work = e->d_work;
     a.order = e->order.p;
     return a;
@@ -558,16 +571,9 @@ static int score_linear(ewk_engine* e, const float* d_pcm, const int64_t* d_off,
     a.out_std = d_std;
     a.out_score = d_score;
     a.out_match = d_match;
-    if (!a.has_template) a.rescore_list = nullptr;
-    {   // (launch_score_f32 zeroes the work counter and the re-score count)
+    {   // (launch_score_f32 zeroes the work and re-score counters; the fp64 re-score runs inside)
         ProfScope ps(e, 0, s);
         HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));
-    }
-    if (a.has_template) {
-        a.f64_scratch = e->f64_scratch.p;
-        a.f64_per_seg = (1 + e->ring_len / HOP) * (NMEL + NMFCC);
-        ProfScope ps(e, 1, s);
-        HIP_TRY(launch_score_f64(e->d_tab64, a, e->f64_grid, nullptr, nullptr, s));
     }
     return EWK_OK;
 }
@@ -614,13 +620,6 @@ int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int
     int rc = check_segments(offsets, lengths, n_seg, n_pcm, &max_len);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(e->device));
-    // grow the fp64 scratch when a host batch holds longer segments than the ring
-    {
-        const int64_t tmax = std::max<int64_t>(1 + e->ring_len / HOP, 1 + max_len / HOP);
-        const int64_t per = tmax * (NMEL + NMFCC);
-        HIP_TRY(hipStreamSynchronize(e->stream));
-        HIP_TRY(e->f64_scratch.reserve((size_t)per * e->f64_grid));
-    }
     HIP_TRY(reserve_rescore(e, n_seg));
     HIP_TRY(e->pcm.reserve(std::max<int64_t>(n_pcm, 1)));
     HIP_TRY(e->offsets.reserve(n_seg));
@@ -645,15 +644,7 @@ int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int
         a.out_score = e->score.p;
         a.out_match = e->match.p;
         a.cand_f32 = (flags & EWK_SCORE_F32_CANDIDATES) ? 1 : 0;
-        if (!a.has_template) a.rescore_list = nullptr;
-        HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));   // (zeroes the work counter and the re-score count)
-        if (a.has_template) {
-            const int64_t tmax = std::max<int64_t>(1 + e->ring_len / HOP, 1 + max_len / HOP);
-            a.f64_scratch = e->f64_scratch.p;
-            a.f64_per_seg = tmax * (NMEL + NMFCC);
-            HIP_TRY(launch_score_f64(e->d_tab64, a, e->f64_grid,
-                                     nullptr, nullptr, s));
-        }
+        HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));   // (zeroes the work and re-score counters)
     }
     if (out_mean) HIP_TRY(hipMemcpyAsync(out_mean, e->mean.p, (size_t)n_seg * NMFCC * 4, hipMemcpyDeviceToHost, s));
     if (out_std) HIP_TRY(hipMemcpyAsync(out_std, e->stdv.p, (size_t)n_seg * NMFCC * 4, hipMemcpyDeviceToHost, s));
@@ -678,10 +669,7 @@ int ewk_score_segments_f64(ewk_engine* e, const float* pcm, int64_t n_pcm, const
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = e->stream;
     HIP_TRY(join_scoring(e, s));
-    const int64_t tmax = std::max<int64_t>(1 + e->ring_len / HOP, 1 + max_len / HOP);
-    const int64_t per = tmax * (NMEL + NMFCC);
-    HIP_TRY(hipStreamSynchronize(s));
-    HIP_TRY(e->f64_scratch.reserve((size_t)per * e->f64_grid));
+    HIP_TRY(reserve_rescore(e, n_seg));
     HIP_TRY(e->pcm.reserve(std::max<int64_t>(n_pcm, 1)));
     HIP_TRY(e->offsets.reserve(n_seg));
     HIP_TRY(e->lengths.reserve(n_seg));
@@ -698,11 +686,13 @@ int ewk_score_segments_f64(ewk_engine* e, const float* pcm, int64_t n_pcm, const
     a.n_seg = n_seg;
     a.out_score = e->score.p;
     a.cand_f32 = (flags & EWK_SCORE_F32_CANDIDATES) ? 1 : 0;
-    a.rescore_list = nullptr;
-    a.rescore_count = nullptr;
-    a.f64_scratch = e->f64_scratch.p;
-    a.f64_per_seg = per;
-    HIP_TRY(launch_score_f64(e->d_tab64, a, e->f64_grid, e->mean64.p, e->std64.p, s));
+    // every segment through the fp64 path: the float32 pass only supplies the speculative
+    // top_db clamp of each segment (its own scores are overwritten)
+    a.list_all = 1;
+    a.rs_slots = e->rs_slots.p;
+    a.out_mean64 = e->mean64.p;
+    a.out_std64 = e->std64.p;
+    HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));
     if (out_mean) HIP_TRY(hipMemcpyAsync(out_mean, e->mean64.p, (size_t)n_seg * NMFCC * 8, hipMemcpyDeviceToHost, s));
     if (out_std) HIP_TRY(hipMemcpyAsync(out_std, e->std64.p, (size_t)n_seg * NMFCC * 8, hipMemcpyDeviceToHost, s));
     if (out_score && e->has_tmpl)
@@ -741,7 +731,7 @@ int ewk_reset_streams(ewk_engine* e) {
         x.last_silent = 1;
     }
     HIP_TRY(hipMemcpyAsync(e->d_st, st.data(), st.size() * sizeof(GateStream), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(e->d_work, 0, 4 * sizeof(int32_t), s));
+    HIP_TRY(hipMemsetAsync(e->d_work, 0, 16 * sizeof(int32_t), s));
     zero_event_state(e);
     HIP_TRY(hipStreamSynchronize(s));
     e->tick = 0;
@@ -763,14 +753,10 @@ static int score_pending(ewk_engine* e, hipStream_t ss, const int32_t* n_events)
     a.ev_base0 = e->ev_base0[e->bank];
     a.n_seg = e->ev_cap;
     a.work = e->d_work + 1;            // ring-mode counters (zeroed at create, re-armed by the tick end)
-    a.rescore_count = e->d_work + 2;
-    // the last workgroup re-scores the near-threshold list in fp64 and advances the watermark
-    // (no second launch per tick)
-    a.adv_done = e->d_work + 3;
+    a.rs_ctl = e->d_work + 8;
+    // the scorer's workgroups re-score the listed segments in fp64 and the last one out advances
+    // the watermark (no second launch per tick)
     a.adv_ev_base = e->evc_bank(e->bank) + 2;
-    a.tab64 = e->d_tab64;
-    a.f64_scratch = e->f64_scratch.p;
-    a.f64_per_seg = (1 + e->sring_len / HOP) * (NMEL + NMFCC);
     HIP_TRY(ensure_poll_region(e));
     a.mirror = e->d_poll + e->bank * kPollRegion;
     a.evc = e->evc_bank(e->bank);

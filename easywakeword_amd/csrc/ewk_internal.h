@@ -60,6 +60,30 @@ struct Tables64 {
 void build_tables(Tables* t);
 void build_tables64(Tables64* t);
 
+// fp64 re-score (csrc/ewk_rescore.h).  A segment the float32 pass cannot decide alone is
+// listed in a slot; its 8-frame chunks are claimed by any wave that has run out of float32
+// work (every scorer workgroup drains the list before it counts itself out, and the last one
+// drains what is left), each chunk's sums land in a part record, and the wave finishing a
+// slot's last chunk combines them in chunk order.
+constexpr int kRsFrames = 8;   // frames per re-score chunk
+struct RsSlot {
+    int32_t seg;       // segment (linear) or event (ring) index
+    int32_t T;         // frames
+    int32_t nclaim;    // claimable units: chunks, or 1 for a serial slot; published last (0 = not ready)
+    int32_t base;      // first part record of the slot (pooled slots)
+    int32_t cursor;    // units claimed (atomic)
+    int32_t done;      // chunks finished (atomic)
+    float theta_s;     // speculative top_db clamp: the float32 pass's log-mel max - 80 dB
+    int32_t serial;    // 1: one wave runs every chunk in order (no part records)
+};
+struct RsPart {                 // one chunk: per coefficient k, rA rB sA sB sAA sAB sBB ([7][20])
+    double v[7 * 20];
+    double mx;                  // log-mel max of the chunk's frames
+    int32_t n;                  // frames
+    int32_t flags;              // 1: a value within the ambiguity window of theta_s, 2: NaN
+};
+static_assert(sizeof(RsPart) % 16 == 0, "part records are 16-B aligned");
+
 // Segment sources for the scorer.
 //   linear: segment i = pcm[offsets[i] : offsets[i] + lengths[i]]
 //   ring  : event i -> ring + stream*ring_len, first sample ring_start, wrap at ring_len
@@ -85,17 +109,20 @@ struct ScoreArgs {
     uint8_t* out_match;
     double threshold;
     double rescore_margin;
-    int32_t* rescore_list;    // indices whose fp32 score fell inside the margin
-    int32_t* rescore_count;
-    int32_t rescore_cap;
     int32_t* order;           // linear mode: work order scratch [n_seg] (longest first), nullptr = index order
-    // ring mode: the last k_score_f32 workgroup out re-scores the listed segments in fp64,
-    // sets *adv_ev_base = *n_events and zeroes *work, *rescore_count and *adv_done
-    int32_t* adv_done;
+    // fp64 re-score (nullptr rs_slots: none).  rs_ctl: [0] slots listed, [1] part records
+    // reserved, [2] scan hint, [3] workgroups out; the last workgroup out zeroes them (and
+    // *work) and, in ring mode, sets *adv_ev_base = *n_events
+    int32_t* rs_ctl;
+    RsSlot* rs_slots;
+    int32_t rs_cap;
+    int32_t rs_part_cap;
+    RsPart* rs_parts;
+    int32_t list_all;         // every segment goes to the fp64 path (ewk_score_segments_f64)
+    double* out_mean64;       // list_all: fp64 statistics [n][20]
+    double* out_std64;
     int32_t* adv_ev_base;
-    const struct Tables64* tab64;   // fp64 re-score tables
-    double* f64_scratch;      // fp64 re-score: [slot][f64_per_seg] log-mel + mfcc rows
-    int64_t f64_per_seg;
+    const struct Tables64* tab64;   // fp64 tables
     // ring mode poll mirror (nullptr: none): the last workgroup copies the bank's counters
     // (evc) and its first min(queued, mirror_chunk) events into pinned host memory
     unsigned char* mirror;
@@ -118,10 +145,6 @@ hipError_t launch_bank_mirror(const int32_t* evc, const ewk_event* ev, uint32_t 
 constexpr int kScoreGridMax = 256;   // one resident workgroup wave of the grid
 constexpr int kScoreGridRing = 256;                     // ring-mode grid (device-side event count)
 int score_grid(int n_seg, int ring_mode);
-// fp64 re-score of rescore_list (device count) or of all n (list == nullptr).
-// (linear batches; ring ticks re-score inside k_score_f32's last workgroup)
-hipError_t launch_score_f64(const Tables64* d_tab64, const ScoreArgs& a, int grid, double* out_mean64,
-                            double* out_std64, hipStream_t s);
 
 // Level-3 pre-processing (ewk_level3.hip): segment i is pcm[offsets[i] ...][:lengths[i]]
 // (linear) or the ring slice of events[i] (ring_len > 0); output at out[out_offsets[i]].

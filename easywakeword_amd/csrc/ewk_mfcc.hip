@@ -140,8 +140,8 @@ constexpr int W_BYTES = W_SPEC + (kSpecOrder + kSpecTiles) * 4;
 constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
 constexpr int LDS_BYTES = L_WG + 16 + 8 * WAVES;
 constexpr int kRescoreFrames = 16;
-constexpr double kTinyMean = 64.0;  // |mean vector| below which linear batches re-score in fp64
-                                    // (loud audio, c0 cancelling: DESIGN.md numerics, "Known gap")
+constexpr double kTinyMean = 64.0;  // |mean vector| below which the fp64 path decides
+                                    // (loud audio, c0 cancelling: DESIGN.md numerics)
 constexpr double kTinyStd = 20.0;   // |std vector| below which the fp64 path decides (bench batch >= 24.8,
                                     // streaming events >= 32.5: scripts/std_norm_dist.py)
 static_assert(LDS_BYTES <= 160 * 1024, "the workgroup must fit a CU's LDS");
@@ -1131,7 +1131,7 @@ __device__ __forceinline__ void work_describe(const WorkCtx& c, WorkAhead& w) {
 template <int RING>
 __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, float* scr, float* tile,
                               float* spec, int lane, const int (&lo)[8], double (&s1)[8], double (&s2)[8],
-                              const WorkCtx& wc, WorkAhead& nx EWK_DBG_PARAM) {
+                              float& theta_out, const WorkCtx& wc, WorkAhead& nx EWK_DBG_PARAM) {
     EWK_TS(tq0);
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     const int T = 1 + v.len / HOP;
@@ -1227,6 +1227,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     // wave-wide log-mel max
     vmax = wave_max(vmax);
     const float theta = vmax - kTopDbUnits;
+    theta_out = theta;
     if (vmin < theta) {
         lds_order();
         for (int cur = 0; cur < ntile; ++cur) {
@@ -1266,7 +1267,8 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
 // Leaves mean / std (fp32-rounded) in misc0[0..19], misc0[20..39] (wave 0's scratch).
 template <int RING>
 __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, float* scr, float* tile,
-                                   float* spec, int wave, int lane, const int (&lo)[8], float* misc0) {
+                                   float* spec, int wave, int lane, const int (&lo)[8], float* misc0,
+                                   float& theta_out) {
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     float* wg_mm = reinterpret_cast<float*>(smem + L_WG + 16);   // [WAVES][2] max, min
     const int T = 1 + v.len / HOP;
@@ -1319,6 +1321,7 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
 #pragma unroll
     for (int w = 0; w < WAVES; ++w) { vmax = fmaxf(vmax, wg_mm[2 * w]); vmin = fminf(vmin, wg_mm[2 * w + 1]); }
     const float theta = vmax - kTopDbUnits;
+    theta_out = theta;
     if (nloc > 0) {
         const int tile_l = wave + WAVES * (nloc - 1);
         if (last_min < theta) {   // the last tile, still in LDS: clamp at the final threshold
@@ -1486,143 +1489,62 @@ __device__ __forceinline__ double score_f32_finish(float uu_m, float uu_s, float
     return (double)(powf(percent, 1.5f) / 10.0f);
 }
 
+#include "ewk_rescore.h"
+
 // Score one segment from its fp32-rounded mean / std (lane k < 20: coefficient k; one wave):
 // wave-parallel dots in a fixed butterfly order, lane 0 finishes the score, writes the
-// decision and queues the segment for the fp64 re-score when it is near the threshold.
+// decision and lists the segment for the fp64 re-score (ewk_rescore.h) when the float32
+// pipeline cannot decide it alone.  theta_s: the float32 pass's log-mel max - 80 dB.
 template <int RING>
 __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, float csf, float tmf, float tsf,
-                                               int lane, int seg, int len, bool& listed) {
-    double score, std2, mean2;
-    if (a.cand_f32) {   // float32 candidates: float products, float-rounded dots (sdot)
-        const float uv_m = (float)wave_sum_d((double)(tmf * cmf)), vv_m = (float)wave_sum_d((double)(cmf * cmf));
-        const float uv_s = (float)wave_sum_d((double)(tsf * csf)), vv_s = (float)wave_sum_d((double)(csf * csf));
-        score = score_f32_finish(a.uu_m32, a.uu_s32, uv_m, vv_m, uv_s, vv_s);
-        std2 = vv_s;
-        mean2 = vv_m;
-    } else {
-        const double uv_m = wave_sum_d((double)tmf * (double)cmf), vv_m = wave_sum_d((double)cmf * (double)cmf);
-        const double uv_s = wave_sum_d((double)tsf * (double)csf), vv_s = wave_sum_d((double)csf * (double)csf);
-        score = score_f64_finish((double)a.uu_m32, (double)a.uu_s32, uv_m, vv_m, uv_s, vv_s);
-        std2 = vv_s;
-        mean2 = vv_m;
-    }
-    if (lane == 0) {
-        const int match = score >= a.threshold;
-        // fp64 re-score: decisions within the margin of the threshold; very short segments
-        // (T <= kRescoreFrames) whose 2..16-frame std vectors are too ill-conditioned for the
-        // float32 pipeline to meet 1e-4; and nearly stationary segments (0 < |std| < kTinyStd:
-        // steady noise, or a few bins above the -100 dB floor: std vectors of norm ~1e-2..20
-        // whose direction the float32 rounding of the MFCCs (~3e-5 absolute) moves by up to
-        // ~3e-4 in the score; scripts/fuzz_err.py over 12 x 200 fuzz segments found 1.3e-4 at
-        // |std| = 8).  An exactly constant segment keeps its NaN (zero std; the reference's own
-        // value there is a rounding artefact).
-        const bool near = fabs(score - a.threshold) < a.rescore_margin || (1 + len / HOP) <= kRescoreFrames ||
-                          (std2 > 0.0 && std2 < kTinyStd * kTinyStd) ||
-                          // linear batches only: a ring tick re-scores its list in one workgroup,
-                          // serially (4 % of a burst's events would cost ~4 ms per tick)
-                          (!RING && mean2 < kTinyMean * kTinyMean);
-        if (RING) {
-            a.events[seg].score = score;
-            a.events[seg].match = match;
-            if (a.mirror) listed = true;   // the last workgroup copies this event to the poll mirror
+                                               int lane, int seg, int len, float theta_s, bool& listed) {
+    bool near = a.list_all;
+    if (a.has_template) {
+        double score, std2, mean2;
+        if (a.cand_f32) {   // float32 candidates: float products, float-rounded dots (sdot)
+            const float uv_m = (float)wave_sum_d((double)(tmf * cmf)), vv_m = (float)wave_sum_d((double)(cmf * cmf));
+            const float uv_s = (float)wave_sum_d((double)(tsf * csf)), vv_s = (float)wave_sum_d((double)(csf * csf));
+            score = score_f32_finish(a.uu_m32, a.uu_s32, uv_m, vv_m, uv_s, vv_s);
+            std2 = vv_s;
+            mean2 = vv_m;
         } else {
-            a.out_score[seg] = score;
-            if (a.out_match) a.out_match[seg] = (uint8_t)match;
+            const double uv_m = wave_sum_d((double)tmf * (double)cmf), vv_m = wave_sum_d((double)cmf * (double)cmf);
+            const double uv_s = wave_sum_d((double)tsf * (double)csf), vv_s = wave_sum_d((double)csf * (double)csf);
+            score = score_f64_finish((double)a.uu_m32, (double)a.uu_s32, uv_m, vv_m, uv_s, vv_s);
+            std2 = vv_s;
+            mean2 = vv_m;
         }
-        if (near && a.rescore_list) {
-            const int slot = atomicAdd(a.rescore_count, 1);
-            if (slot < a.rescore_cap) a.rescore_list[slot] = seg;
-            listed = true;   // (lane 0) this wave queued a segment for the fp64 re-score
+        if (lane == 0) {
+            const int match = score >= a.threshold;
+            // fp64 re-score: decisions within the margin of the threshold; very short segments
+            // (T <= kRescoreFrames) whose 2..16-frame std vectors are too ill-conditioned for the
+            // float32 pipeline to meet 1e-4; nearly stationary segments (0 < |std| < kTinyStd:
+            // steady noise, or a few bins above the -100 dB floor: std vectors of norm ~1e-2..20
+            // whose direction the float32 rounding of the MFCCs (~3e-5 absolute) moves by up to
+            // ~3e-4 in the score; scripts/fuzz_err.py over 12 x 200 fuzz segments found 1.3e-4 at
+            // |std| = 8); and loud segments whose MFCC mean vector nearly vanishes (|mean| <
+            // kTinyMean: c0's positive and negative frames cancel, the float32 log-mel error
+            // becomes a direction error, up to 3.6e-4 in the score; DESIGN.md numerics).  An
+            // exactly constant segment keeps its NaN (zero std; the reference's own value there
+            // is a rounding artefact).
+            near = near || fabs(score - a.threshold) < a.rescore_margin || (1 + len / HOP) <= kRescoreFrames ||
+                   (std2 > 0.0 && std2 < kTinyStd * kTinyStd) || mean2 < kTinyMean * kTinyMean;
+            if (RING) {
+                a.events[seg].score = score;
+                a.events[seg].match = match;
+                if (a.mirror) listed = true;   // the last workgroup copies this event to the poll mirror
+            } else {
+                a.out_score[seg] = score;
+                if (a.out_match) a.out_match[seg] = (uint8_t)match;
+            }
         }
+    }
+    if (lane == 0 && near && a.rs_slots) {
+        rs_list(a, seg, len, theta_s);
+        listed = true;   // (lane 0) this wave listed a segment for the fp64 re-score
     }
 }
 
-// LDS of the fp64 re-score (k_score_f64's static arrays, or carved from k_score_f32's
-// dynamic LDS in the ring-mode tick end)
-struct F64Lds {
-    double2* z;      // [NW][256]
-    double* p;       // [NW][NBIN + 3]
-    double* win;     // [NFFT]
-    double2* tw;     // [128]
-    double2* cs;     // [NBIN]
-    double* dct;     // [NMFCC * NMEL]
-    float* mw;       // [2 * NBIN + 2 * NMEL]
-    int* mlo;        // [NMEL]
-    int* moff;       // [NMEL + 1]
-    double* red;     // [NW]
-    double* stat;    // [2 * NMFCC]
-};
-template <int RING, int NW>
-__device__ __forceinline__ void score_f64_body(const Tables64* __restrict__ tb, const ScoreArgs& a, double* lm, double* out_mean64,
-                               double* out_std64, int first, int count, int stride, const F64Lds& L);
-
-// Ring-mode tick end, run by every workgroup of a k_score_f32 ring launch after its last
-// segment: the last workgroup out re-scores the near-threshold list in fp64 (its 8 waves
-// take the frames in turn; the list is short -- usually empty) and advances the event
-// watermark for the next tick.  Writers publish with a device-scope release before their
-// arrival count: only a workgroup that queued a segment has anything the last one reads or
-// overwrites (the list entry, the event's fp32 score), so only such a workgroup pays the
-// device-scope release (an L2 write-back); the count and the list are read with agent-scope
-// atomic loads.  `listed`: lane 0 of a wave that queued a segment.
-template <int RING>
-__device__ void ring_tick_end(const ScoreArgs& a, unsigned char* smem, bool listed) {
-    int* flag = reinterpret_cast<int*>(smem + L_WG);   // [0] last, [1 + wave] listed
-    const int wave = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) flag[1 + wave] = listed;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int any = 0;
-        for (int w = 0; w < WAVES; ++w) any |= flag[1 + w];
-        if (any) __threadfence();
-        flag[0] = __hip_atomic_fetch_add(a.adv_done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
-    }
-    __syncthreads();
-    int* last = flag;
-    if (!last[0]) return;
-    const int n = a.rescore_list ? min(__hip_atomic_load(a.rescore_count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                       a.rescore_cap)
-                                 : 0;
-    if (n > 0) {
-        unsigned char* q = smem;
-        F64Lds L;
-        L.z = reinterpret_cast<double2*>(q);   q += WAVES * 256 * sizeof(double2);
-        L.p = reinterpret_cast<double*>(q);    q += WAVES * (NBIN + 3) * sizeof(double);
-        L.win = reinterpret_cast<double*>(q);  q += NFFT * sizeof(double);
-        L.tw = reinterpret_cast<double2*>(q);  q += 128 * sizeof(double2);
-        L.cs = reinterpret_cast<double2*>(q);  q += NBIN * sizeof(double2);
-        L.dct = reinterpret_cast<double*>(q);  q += NMFCC * NMEL * sizeof(double);
-        L.red = reinterpret_cast<double*>(q);  q += WAVES * sizeof(double);
-        L.stat = reinterpret_cast<double*>(q); q += 2 * NMFCC * sizeof(double);
-        L.mw = reinterpret_cast<float*>(q);    q += (2 * NBIN + 2 * NMEL) * sizeof(float);
-        L.mlo = reinterpret_cast<int*>(q);     q += NMEL * sizeof(int);
-        L.moff = reinterpret_cast<int*>(q);
-        score_f64_body<RING, WAVES>(a.tab64, a, a.f64_scratch, nullptr, nullptr, 0, n, 1, L);
-    }
-    if (threadIdx.x == 0) {
-        *a.adv_ev_base = *a.n_events;
-        *a.work = 0;
-        *a.rescore_count = 0;
-        *a.adv_done = 0;
-        __threadfence();
-    }
-    if (a.mirror) {   // poll mirror: the bank's counters and first events -> pinned host memory
-        __syncthreads();   // this workgroup's re-score writes are done and fenced by thread 0
-        const volatile int32_t* vc = a.evc;
-        const uint4 c = make_uint4((uint32_t)vc[0], (uint32_t)vc[1], (uint32_t)vc[2], (uint32_t)vc[3]);
-        const int32_t n = (int32_t)min(min((uint32_t)(c.x - (uint32_t)a.ev_base0), (uint32_t)a.n_seg),
-                                       (uint32_t)a.mirror_chunk);
-        if (threadIdx.x == 0) *reinterpret_cast<uint4*>(a.mirror) = c;
-        const uint4* src = reinterpret_cast<const uint4*>(a.events);
-        uint4* dst = reinterpret_cast<uint4*>(a.mirror + 16);
-        const int nq = n * (int)(sizeof(ewk_event) / 16);
-        // every workgroup that wrote a score released it before its arrival count, and thread
-        // 0's device-scope fence above (after the last arrival) acquired them for this workgroup
-        for (int i = threadIdx.x; i < nq; i += blockDim.x) dst[i] = src[i];
-    }
-}
-static_assert(WAVES * 256 * 16 + WAVES * (NBIN + 3) * 8 + NFFT * 8 + 128 * 16 + NBIN * 16 + NMFCC * NMEL * 8 +
-                  WAVES * 8 + 2 * NMFCC * 8 + (2 * NBIN + 2 * NMEL) * 4 + (2 * NMEL + 1) * 4 <= L_WG,
-              "the fp64 re-score carve must end below the ring-mode flag");
 
 // MODE 0: linear batch; 1: ring events, one segment per workgroup (cooperative); 2: ring
 // events, one segment per wave from the work counter.  S16: int16 rings (EWK_RING_I16).
@@ -1645,7 +1567,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
         // one segment per workgroup: a workgroup without one skips the table fill (most of
         // a quiet tick's 256 workgroups)
         if (MODE == 1 && (int)blockIdx.x >= r_count) {
-            ring_tick_end<RING>(a, smem, false);
+            score_tail<RING>(a, smem, false);
             return;
         }
     }
@@ -1725,7 +1647,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
     // the template is loop-invariant: fetched once, off every segment's critical path.
     // (Reserving the next work item ahead was tried: the tail imbalance costs more.)
     const bool act = lane < NMFCC;
-    bool listed = false;   // lane 0: this wave queued a segment for the fp64 re-score (ring tick end)
+    bool listed = false;   // lane 0: this wave listed a segment for the fp64 re-score (score_tail)
     const float tmf = (a.has_template && act) ? a.tmpl[lane] : 0.0f;
     const float tsf = (a.has_template && act) ? a.tmpl[NMFCC + lane] : 0.0f;
     // Ring mode, MODE 1 (a tick of ~10^3-10^4 streams: a few hundred segments, latency
@@ -1748,16 +1670,17 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
                 const SegSrc<RING> v = make_src<RING>(
                     static_cast<const unsigned char*>(ring_base) + (int64_t)ev.stream * a.ring_len * sample_bytes(RING),
                     ev.ring_start, a.ring_len, ev.length);
-                segment_stats_coop(v, smem, scr, tile, spec, wave, lane, lo, misc0);
-                if (wave == 0 && a.has_template)
+                float theta_s;
+                segment_stats_coop(v, smem, scr, tile, spec, wave, lane, lo, misc0, theta_s);
+                if (wave == 0 && (a.has_template || a.list_all))
                     score_epilogue<RING>(a, act ? misc0[lane] : 0.0f, act ? misc0[20 + lane] : 0.0f, tmf, tsf, lane,
-                                         seg, v.len, listed);
+                                         seg, v.len, theta_s, listed);
             }
             if (threadIdx.x == 0) wg_idx[0] = nxt;
             __syncthreads();
             idx = wg_idx[0];
         }
-        ring_tick_end<RING>(a, smem, listed);
+        score_tail<RING>(a, smem, listed);
         return;
     }
 #ifdef EWK_TIMING
@@ -1789,7 +1712,8 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
         EWK_TADD(0, tw0, tw1);
 
         double st1[8], st2[8];
-        segment_stats(v, smem, scr, tile, spec, lane, lo, st1, st2, wc, nx EWK_DBG_ARG);
+        float theta_s;
+        segment_stats(v, smem, scr, tile, spec, lane, lo, st1, st2, theta_s, wc, nx EWK_DBG_ARG);
         EWK_TS(tw2);
 
         // ---- lane k < 20 holds coefficient k's mean / std (fp32-rounded like the reference's)
@@ -1798,7 +1722,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
             if (a.out_mean) a.out_mean[(int64_t)seg * NMFCC + lane] = cmf;
             if (a.out_std) a.out_std[(int64_t)seg * NMFCC + lane] = csf;
         }
-        if (a.has_template) score_epilogue<RING>(a, cmf, csf, tmf, tsf, lane, seg, v.len, listed);
+        if (a.has_template || a.list_all) score_epilogue<RING>(a, cmf, csf, tmf, tsf, lane, seg, v.len, theta_s, listed);
         lds_order();
         EWK_TS(tw3);
         EWK_TADD(7, tw2, tw3);
@@ -1811,7 +1735,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
     if (lane == 0)
         for (int k = 0; k < kDbgN; ++k) atomicAdd(&g_ewk_dbg[k], (unsigned long long)dbg[k]);
 #endif
-    if (RING) ring_tick_end<RING>(a, smem, listed);
+    score_tail<RING>(a, smem, listed);
 }
 
 #ifdef EWK_TIMING
@@ -1886,11 +1810,11 @@ __global__ __launch_bounds__(kLptBlock) void k_lpt_hist(const int32_t* __restric
 
 __global__ __launch_bounds__(kLptBlock) void k_lpt_scatter(const int32_t* __restrict__ lengths, int32_t n,
                                                            int32_t* __restrict__ order, int32_t* __restrict__ cnt,
-                                                           int32_t* __restrict__ work, int32_t* __restrict__ rescore_count) {
+                                                           int32_t* __restrict__ work, int32_t* __restrict__ rs_ctl) {
     __shared__ int h[kLptBuckets], base[kLptBuckets];
     if (blockIdx.x == 0 && threadIdx.x == 0) {   // the scorer's counters (no fill launches)
         *work = 0;
-        if (rescore_count) *rescore_count = 0;
+        for (int i = 0; i < 4; ++i) rs_ctl[i] = 0;
     }
     if (threadIdx.x < kLptBuckets) h[threadIdx.x] = 0;
     __syncthreads();
@@ -1921,7 +1845,7 @@ int score_grid(int n_seg, int ring_mode) {
 hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mode, hipStream_t s) {
     if (a.n_seg <= 0) return hipSuccess;
     const int grid = score_grid(a.n_seg, ring_mode);
-    if (ring_mode) {   // ring mode: the re-score launch re-arms the counter after each tick
+    if (ring_mode) {   // ring mode: the last workgroup out re-arms the counters after each tick
         if (ring_mode == 2 && a.pcm16) hipLaunchKernelGGL((k_score_f32<2, 1>), dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
         else if (ring_mode == 2) hipLaunchKernelGGL((k_score_f32<2, 0>), dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
         else if (a.pcm16) hipLaunchKernelGGL((k_score_f32<1, 1>), dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, a);
@@ -1936,254 +1860,15 @@ hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mo
             const int g = std::min(256, (a.n_seg + kLptBlock - 1) / kLptBlock);
             hipLaunchKernelGGL(k_lpt_hist, dim3(g), dim3(kLptBlock), 0, s, a.lengths, a.n_seg, cnt);
             hipLaunchKernelGGL(k_lpt_scatter, dim3(g), dim3(kLptBlock), 0, s, a.lengths, a.n_seg, a.order, cnt, a.work,
-                               a.rescore_count);
+                               a.rs_ctl);
         } else {
             b.order = nullptr;
             hipError_t e = hipMemsetAsync(a.work, 0, sizeof(int32_t), s);
-            if (e == hipSuccess && a.rescore_count) e = hipMemsetAsync(a.rescore_count, 0, sizeof(int32_t), s);
+            if (e == hipSuccess) e = hipMemsetAsync(a.rs_ctl, 0, 4 * sizeof(int32_t), s);
             if (e != hipSuccess) return e;
         }
         hipLaunchKernelGGL((k_score_f32<0, 0>), dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, b);
     }
-    return hipGetLastError();
-}
-
-// ============================================================================
-// fp64 reference-precision path (re-scoring near the decision threshold).
-// One 256-thread workgroup per segment; fp64 FFT per frame with the float32-
-// rounded librosa mel basis, fp64 log10, top_db clamp, fp64 DCT and two-pass
-// mean/std -- the float64 candidate path of the reference (wakeword.py:1105-1121
-// hands float64 ring slices to librosa).
-// ============================================================================
-// numpy's float64 pairwise add.reduce over n strided values (n <= 8192: one ufunc buffer)
-struct SegView {
-    const float* p;   // linear: segment base; ring: stream ring base (float32) ...
-    const int16_t* p16;   // ... or int16 ring base (EWK_RING_I16)
-    int64_t start;    // ring: physical index of sample 0
-    int64_t ring;     // 0 = linear
-    int32_t len;
-};
-
-__device__ __forceinline__ float seg_sample(const SegView& v, int q) {
-    if (q < 0 || q >= v.len) return 0.0f;
-    int64_t idx = v.start + q;
-    if (v.ring && idx >= v.ring) idx -= v.ring;
-    return v.p16 ? (float)v.p16[idx] * (1.0f / 32768.0f) : v.p[idx];
-}
-
-__device__ double pw_sum(const double* a, int n, int stride) {
-    if (n < 8) {
-        double r = 0.0;
-        for (int i = 0; i < n; ++i) r += a[i * stride];
-        return r;
-    }
-    if (n <= 128) {
-        double r[8];
-        for (int j = 0; j < 8; ++j) r[j] = a[j * stride];
-        int i = 8;
-        const int lim = n - (n % 8);
-        for (; i < lim; i += 8)
-            for (int j = 0; j < 8; ++j) r[j] += a[(i + j) * stride];
-        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
-        for (; i < n; ++i) res += a[i * stride];
-        return res;
-    }
-    int n2 = n / 2;
-    n2 -= n2 % 8;
-    return pw_sum(a, n2, stride) + pw_sum(a + (int64_t)n2 * stride, n - n2, stride);
-}
-
-__device__ double np_sum(const double* a, int n, int stride) {
-    double acc = 0.0;
-    for (int c = 0; c < n; c += 8192) acc += pw_sum(a + (int64_t)c * stride, min(8192, n - c), stride);
-    return acc;
-}
-
-// Wave-level radix-2 FFT of 256 complex doubles held in LDS in bit-reversed order
-// (the 512-point real frame as z[n] = x[2n] + i x[2n+1]); tw[k] = W256^k, k < 128.
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ void fft256_f64(double2* z, const double2* tw, int lane) {
-#pragma unroll 1
-    for (int s = 0; s < 8; ++s) {
-        const int half = 1 << s;
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int b = lane + 64 * j;                  // butterfly 0..127
-            const int pos = b & (half - 1);
-            const int i0 = ((b >> s) << (s + 1)) + pos, i1 = i0 + half;
-            const double2 w = tw[pos << (7 - s)];
-            const double2 u = z[i0], v = z[i1];
-            const double tr = v.x * w.x - v.y * w.y, ti = v.x * w.y + v.y * w.x;
-            z[i0] = make_double2(u.x + tr, u.y + ti);
-            z[i1] = make_double2(u.x - tr, u.y - ti);
-        }
-        wave_sync();
-    }
-}
-
-// One 256-thread workgroup per segment; its four waves take the frames in turn (fp64
-// FFT, packed-support mel, log10), then the workgroup clamps at max - 80 dB, runs the
-// fp64 DCT and numpy's pairwise mean / population std.
-template <int RING, int NW>
-__device__ __forceinline__ void score_f64_body(const Tables64* __restrict__ tb, const ScoreArgs& a, double* lm,
-                                               double* out_mean64, double* out_std64, int first, int count, int stride,
-                                               const F64Lds& L) {
-    constexpr int NT = 64 * NW;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    double* s_win = L.win;
-    double2* s_tw = L.tw;
-    double2* s_cs = L.cs;
-    double* s_dct = L.dct;
-    float* s_mw = L.mw;
-    int* s_mlo = L.mlo;
-    int* s_moff = L.moff;
-    double* s_red = L.red;
-    double* s_stat = L.stat;
-    for (int i = tid; i < NFFT; i += NT) s_win[i] = tb->win[i];
-    for (int i = tid; i < 128; i += NT) s_tw[i] = make_double2(tb->cs[2 * i], -tb->sn[2 * i]);   // W256^i = W512^2i
-    for (int i = tid; i < NBIN; i += NT) s_cs[i] = make_double2(tb->cs[i], tb->sn[i]);
-    for (int i = tid; i < NMFCC * NMEL; i += NT) s_dct[i] = tb->dct[i];
-    for (int i = tid; i < 2 * NBIN + 2 * NMEL; i += NT) s_mw[i] = tb->mel_w[i];
-    for (int i = tid; i < NMEL; i += NT) s_mlo[i] = tb->mel_lo[i];
-    for (int i = tid; i <= NMEL; i += NT) s_moff[i] = tb->mel_off[i];
-    __syncthreads();
-    // lm: this workgroup's [T][128] log-mel, then [T][20] mfcc
-    double2* z = L.z + 256 * wave;
-    double* pw = L.p + (NBIN + 3) * wave;
-    for (int w = first; w < count; w += stride) {
-        const int seg = a.rescore_list ? __hip_atomic_load(a.rescore_list + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : w;
-        SegView v;
-        if (RING) {
-            const ewk_event ev = a.events[seg];
-            v.p = a.pcm ? a.pcm + (int64_t)ev.stream * a.ring_len : nullptr;
-            v.p16 = a.pcm16 ? a.pcm16 + (int64_t)ev.stream * a.ring_len : nullptr;
-            v.start = ev.ring_start;
-            v.ring = a.ring_len;
-            v.len = ev.length;
-        } else {
-            v.p = a.pcm;
-            v.p16 = nullptr;
-            v.start = a.offsets[seg];
-            v.ring = 0;
-            v.len = a.lengths[seg];
-        }
-        const int T = 1 + v.len / HOP;
-        if ((int64_t)T * (NMEL + NMFCC) > a.f64_per_seg) continue;   // host sizes scratch; never expected
-        double lmax = -INFINITY;
-        for (int t = wave; t < T; t += NW) {
-            // windowed z[n] = x[2n] + i x[2n+1], stored bit-reversed for the in-place FFT
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int n = lane + 64 * j;
-                const int q = t * HOP - NFFT / 2 + 2 * n;
-                z[__brev((unsigned)n) >> 24] = make_double2(s_win[2 * n] * (double)seg_sample(v, q),
-                                                            s_win[2 * n + 1] * (double)seg_sample(v, q + 1));
-            }
-            wave_sync();
-            fft256_f64(z, s_tw, lane);
-            // untangle: X[k] = E[k] + W512^k O[k], E = (Z[k] + conj Z[256-k]) / 2,
-            // O = (Z[k] - conj Z[256-k]) / 2i;  P[k] = |X[k]|^2, k = 0..256
-            for (int k = lane; k < NBIN; k += 64) {
-                const double2 zk = z[k & 255], zc = z[(256 - k) & 255];
-                const double er = 0.5 * (zk.x + zc.x), ei = 0.5 * (zk.y - zc.y);
-                const double orr = 0.5 * (zk.y + zc.y), oi = -0.5 * (zk.x - zc.x);
-                const double2 cs = s_cs[k];   // W512^k = cos - i sin
-                const double xr = er + (orr * cs.x + oi * cs.y);
-                const double xi = ei + (oi * cs.x - orr * cs.y);
-                pw[k] = xr * xr + xi * xi;
-            }
-            wave_sync();
-            // mel (every non-zero weight of the band, in bin order: the dense dot's value)
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int m = lane + 64 * h;
-                const int lo = s_mlo[m], o0 = s_moff[m], o1 = s_moff[m + 1];
-                double acc = 0.0;
-                for (int o = o0; o < o1; ++o) acc = fma((double)s_mw[o], pw[lo + o - o0], acc);
-                const double db = 10.0 * log10(acc < 1e-10 ? 1e-10 : acc);   // np.maximum: NaN propagates
-                lm[(int64_t)t * NMEL + m] = db;
-                lmax = fmax(lmax, db);
-            }
-            wave_sync();
-        }
-        for (int o = 32; o > 0; o >>= 1) lmax = fmax(lmax, __shfl_xor(lmax, o, 64));
-        if (lane == 0) s_red[wave] = lmax;
-        __syncthreads();
-        double mx = s_red[0];
-        for (int w2 = 1; w2 < NW; ++w2) mx = fmax(mx, s_red[w2]);
-        const double theta = mx - 80.0;
-        double* mf = lm + (int64_t)T * NMEL;
-        for (int i = tid; i < T * NMFCC; i += NT) {
-            const int t = i / NMFCC, k = i % NMFCC;
-            const double* row = lm + (int64_t)t * NMEL;
-            const double* dk = s_dct + k * NMEL;
-            double acc = 0.0;
-            for (int m = 0; m < NMEL; ++m) acc = fma(dk[m], row[m] < theta ? theta : row[m], acc);
-            mf[i] = acc;
-        }
-        __syncthreads();
-        if (tid < NMFCC) {   // np.mean / np.std(axis=1): pairwise sums, population std
-            const double mean = np_sum(mf + tid, T, NMFCC) / T;
-            for (int t = 0; t < T; ++t) { const double d = mf[t * NMFCC + tid] - mean; mf[t * NMFCC + tid] = d * d; }
-            const double sd = sqrt(np_sum(mf + tid, T, NMFCC) / T);
-            s_stat[tid] = mean;
-            s_stat[NMFCC + tid] = sd;
-            if (out_mean64) { out_mean64[(int64_t)seg * NMFCC + tid] = mean; out_std64[(int64_t)seg * NMFCC + tid] = sd; }
-        }
-        __syncthreads();
-        if (tid == 0 && a.has_template) {
-            double score;
-            if (a.cand_f32) {
-                float c32[2 * NMFCC];
-                for (int i = 0; i < 2 * NMFCC; ++i) c32[i] = (float)s_stat[i];
-                score = score_f32cand(a.tmpl, a.tmpl + NMFCC, c32, c32 + NMFCC);
-            } else {
-                score = score_f64cand(a.tmpl, a.tmpl + NMFCC, s_stat, s_stat + NMFCC);
-            }
-            const int match = score >= a.threshold;
-            if (RING) {
-                a.events[seg].score = score;
-                a.events[seg].match = match;
-                if (a.rescore_list) a.events[seg].flags |= EWK_EV_RESCORED;
-            } else {
-                if (a.out_score) a.out_score[seg] = score;
-                if (a.out_match) a.out_match[seg] = (uint8_t)match;
-            }
-        }
-        __syncthreads();
-    }
-}
-
-template <int RING>
-__global__ __launch_bounds__(256) void k_score_f64(const Tables64* __restrict__ tb, ScoreArgs a,
-                                                   double* out_mean64, double* out_std64) {
-    __shared__ double2 s_z[4][256];
-    __shared__ double s_p[4][NBIN + 3];
-    __shared__ double s_win[NFFT];
-    __shared__ double2 s_tw[128];          // W256^k
-    __shared__ double2 s_cs[NBIN];         // (cos, sin)(2 pi k / 512), k <= 256
-    __shared__ double s_dct[NMFCC * NMEL];
-    __shared__ float s_mw[2 * NBIN + 2 * NMEL];
-    __shared__ int s_mlo[NMEL], s_moff[NMEL + 1];
-    __shared__ double s_red[4];
-    __shared__ double s_stat[2 * NMFCC];
-    const F64Lds L = {&s_z[0][0], &s_p[0][0], s_win, s_tw, s_cs, s_dct, s_mw, s_mlo, s_moff, s_red, s_stat};
-    int count;
-    if (a.rescore_list) count = min(*a.rescore_count, a.rescore_cap);
-    else count = RING ? min(a.n_seg, (int)((uint32_t)*a.n_events - (uint32_t)a.ev_base0)) : a.n_seg;
-    if ((int)blockIdx.x < count)
-        score_f64_body<RING, 4>(tb, a, a.f64_scratch + (int64_t)blockIdx.x * a.f64_per_seg, out_mean64, out_std64,
-                                (int)blockIdx.x, count, (int)gridDim.x, L);
-}
-hipError_t launch_score_f64(const Tables64* d_tab64, const ScoreArgs& a, int grid, double* out_mean64,
-                            double* out_std64, hipStream_t s) {
-    if (grid <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_score_f64<0>, dim3(grid), dim3(256), 0, s, d_tab64, a, out_mean64, out_std64);
     return hipGetLastError();
 }
 

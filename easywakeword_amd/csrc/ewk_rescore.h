@@ -1,0 +1,622 @@
+// ewk_rescore.h -- the fp64 re-score of the segments the float32 pass cannot decide alone
+// (near the threshold, very short, nearly stationary, or with a vanishing MFCC mean vector:
+// see score_epilogue), run by k_score_f32's own workgroups after their float32 work.
+// Included by ewk_mfcc.hip after the score arithmetic; device code only.
+//
+// This is the float64 candidate path of the reference (wakeword.py:509-513 hands float64 ring
+// slices to WordMatcher.extract_mfcc, wakeword.py:544-567 -> librosa 0.11.0 feature.mfcc with
+// complex128 stft, float32 Slaney weights, float64 power_to_db and DCT, numpy mean / std).
+//
+// Work split.  A listed segment is a slot; its frames are cut into 8-frame chunks that any
+// wave out of float32 work claims (every workgroup drains the list before it counts itself
+// out; the last one out drains what is left, so no workgroup ever waits on another).  One
+// chunk = one wave, one frame at a time over its 64 lanes:
+//   samples -> windowed z[n] = w[2n] x[2n] + i w[2n+1] x[2n+1] (lane j: n = j + 64 r)
+//   -> radix-4 Stockham FFT (Ns = 1, 4, 16, 64; LDS between iterations, natural order out)
+//   -> real-FFT untangle + power (partner bin 256 - k through LDS) -> Slaney bands over each
+//   band's packed support -> 10 log10(max(1e-10, .)) into the chunk's log-mel tile.
+// top_db couples every frame to the segment's max; the chunk does not know it yet.  So the
+// DCT is split by a speculative clamp theta_s (the float32 pass's max - 80 dB):
+//   c_k = A_k + theta B_k,  A_k = sum_{x >= theta} D_km x_m,  B_k = sum_{x < theta} D_km,
+// exact for the true theta as long as no value lies within kRsWindow of theta_s (then the
+// classification x >= theta_s equals x >= theta); a chunk holding such a value is recomputed
+// with the exact theta by the wave that finishes the slot (rare: ~0.1 value per segment).
+// The chunk's sums (shifted by its first frame: identical frames give an exact 0 std) go to
+// a part record; the finishing wave merges the parts in chunk order as polynomials in theta,
+// so the result does not depend on which waves ran which chunks (MODE 0, 1, 2 and the
+// serial fallback give the same bits).
+//
+// scripts/f64_chunk_model.py is the numpy model of these index maps and algebra.
+
+constexpr double kRsWindow = 1e-3;   // dB; the float32 max is within ~1e-5 dB of the fp64 one
+constexpr double kRsTopDb = 80.0;
+
+// What the drain needs of ScoreArgs, copied in score_tail: the drain is a real call (its
+// registers are its own), and a reference to the kernel's own ScoreArgs would make the
+// compiler copy the whole kernarg block to scratch and read every field from there in the
+// float32 hot loop as well.
+struct RsArgs {
+    const float* pcm;
+    const int16_t* pcm16;
+    const int64_t* offsets;
+    const int32_t* lengths;
+    ewk_event* events;
+    int64_t ring_len;
+    const float* tmpl;
+    double threshold;
+    int32_t has_template;
+    int32_t cand_f32;
+    int32_t* rs_ctl;
+    RsSlot* rs_slots;
+    RsPart* rs_parts;
+    int32_t rs_cap;
+    double* out_score;
+    uint8_t* out_match;
+    double* out_mean64;
+    double* out_std64;
+    const Tables64* tab64;
+};
+
+__device__ __forceinline__ RsArgs rs_args(const ScoreArgs& a) {
+    RsArgs r;
+    r.pcm = a.pcm; r.pcm16 = a.pcm16; r.offsets = a.offsets; r.lengths = a.lengths; r.events = a.events;
+    r.ring_len = a.ring_len; r.tmpl = a.tmpl; r.threshold = a.threshold; r.has_template = a.has_template;
+    r.cand_f32 = a.cand_f32; r.rs_ctl = a.rs_ctl; r.rs_slots = a.rs_slots; r.rs_parts = a.rs_parts;
+    r.rs_cap = a.rs_cap; r.out_score = a.out_score; r.out_match = a.out_match; r.out_mean64 = a.out_mean64;
+    r.out_std64 = a.out_std64; r.tab64 = a.tab64;
+    return r;
+}
+
+// LDS of the re-score (the float32 tables and scratch are dead by then; ends below L_WG)
+constexpr int RS_D = 0;                                     // double [NMEL][NMFCC]
+constexpr int RS_MLO = RS_D + NMEL * NMFCC * 8;             // int [NMEL]
+constexpr int RS_MOFF = RS_MLO + NMEL * 4;                  // int [NMEL + 1]
+constexpr int RS_MW = RS_MOFF + (NMEL + 4) * 4;             // float [2 NBIN + 2 NMEL]
+constexpr int RS_WAVES = (RS_MW + (2 * NBIN + 2 * NMEL) * 4 + 15) & ~15;
+constexpr int RS_BUF = 0;                                   // per wave: double2 [256] FFT / double P[257]
+constexpr int RS_XA = 256 * 16;                             // double [NMEL][kRsFrames]: x or 0 (clamped)
+constexpr int RS_XB = RS_XA + NMEL * kRsFrames * 8;         // float [NMEL][kRsFrames]: 0 or 1 (clamped)
+constexpr int RS_WAVE_BYTES = RS_XB + NMEL * kRsFrames * 4;
+static_assert(RS_WAVES + WAVES * RS_WAVE_BYTES <= L_WG, "the re-score carve must end below the workgroup flags");
+static_assert(NMFCC == 20 && kRsFrames == 8, "the DCT lane split assumes 20 coefficients and 8-frame chunks");
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// A segment's samples for the fp64 path (linear batch or wrap-aware ring slice).
+struct SegView {
+    const float* p;       // linear: the batch base; ring: stream ring base (float32) ...
+    const int16_t* p16;   // ... or int16 ring base (EWK_RING_I16)
+    int64_t start;        // linear: segment offset; ring: physical index of sample 0
+    int64_t ring;         // 0 = linear
+    int32_t len;
+};
+
+__device__ __forceinline__ float seg_sample(const SegView& v, int q) {
+    if (q < 0 || q >= v.len) return 0.0f;   // stft(center=True, pad_mode='constant')
+    int64_t idx = v.start + q;
+    if (v.ring && idx >= v.ring) idx -= v.ring;
+    return v.p16 ? (float)v.p16[idx] * (1.0f / 32768.0f) : v.p[idx];
+}
+
+template <int RING>
+__device__ __forceinline__ SegView rs_view(const RsArgs& a, int seg) {
+    SegView v;
+    if (RING) {
+        const ewk_event ev = a.events[seg];
+        v.p = a.pcm ? a.pcm + (int64_t)ev.stream * a.ring_len : nullptr;
+        v.p16 = a.pcm16 ? a.pcm16 + (int64_t)ev.stream * a.ring_len : nullptr;
+        v.start = ev.ring_start;
+        v.ring = a.ring_len;
+        v.len = ev.length;
+    } else {
+        v.p = a.pcm;
+        v.p16 = nullptr;
+        v.start = a.offsets[seg];
+        v.ring = 0;
+        v.len = a.lengths[seg];
+    }
+    return v;
+}
+
+// Per-lane constants of the frame pipeline (from the fp64 tables in global memory, L2-hot).
+struct RsLane {
+    double win[8];    // w[2n], w[2n+1] for n = lane + 64 r
+    double2 tw[9];    // Stockham twiddles W_{4 Ns}^{r (lane % Ns)}, Ns = 4, 16, 64, r = 1..3
+    double2 tu[4];    // untangle (cos, sin)(2 pi k / 512), k = lane + 64 r
+};
+
+__device__ __forceinline__ void rs_lane_init(const Tables64* __restrict__ tb, int lane, RsLane& c) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int n = lane + 64 * r;
+        c.win[2 * r] = tb->win[2 * n];
+        c.win[2 * r + 1] = tb->win[2 * n + 1];
+        c.tu[r] = make_double2(tb->cs[n], tb->sn[n]);
+    }
+#pragma unroll
+    for (int it = 0; it < 3; ++it) {
+        const int lg = 2 * it + 2, e = lane & ((1 << lg) - 1);   // Ns = 4 << (2 it)
+#pragma unroll
+        for (int r = 1; r < 4; ++r) {
+            const int idx = ((128 >> lg) * r * e) & (NFFT - 1);  // W_{4 Ns}^{r e} = W_512^{(128 / Ns) r e}
+            c.tw[3 * it + r - 1] = make_double2(tb->cs[idx], -tb->sn[idx]);
+        }
+    }
+}
+
+__device__ __forceinline__ double2 zmul(double2 a, double2 w) {
+    return make_double2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
+}
+
+// The WG-shared tables: the DCT as [m][k] (lanes of one band read 20 consecutive doubles)
+// and the Slaney bands' packed support.
+__device__ void rs_load_tables(const Tables64* __restrict__ tb, unsigned char* smem) {
+    double* D = reinterpret_cast<double*>(smem + RS_D);
+    int* mlo = reinterpret_cast<int*>(smem + RS_MLO);
+    int* moff = reinterpret_cast<int*>(smem + RS_MOFF);
+    float* mw = reinterpret_cast<float*>(smem + RS_MW);
+    for (int i = threadIdx.x; i < NMEL * NMFCC; i += blockDim.x) {
+        const int m = i / NMFCC, k = i % NMFCC;
+        D[i] = tb->dct[k * NMEL + m];
+    }
+    for (int i = threadIdx.x; i < NMEL; i += blockDim.x) mlo[i] = tb->mel_lo[i];
+    for (int i = threadIdx.x; i <= NMEL; i += blockDim.x) moff[i] = tb->mel_off[i];
+    for (int i = threadIdx.x; i < 2 * NBIN + 2 * NMEL; i += blockDim.x) mw[i] = tb->mel_w[i];
+}
+
+// One frame t of the segment -> column f of the chunk's log-mel tile (split at theta_s),
+// with the running max, the ambiguity flag (|x - theta_s| <= W) and the NaN flag.
+__device__ __forceinline__ void rs_frame(const SegView& v, int t, const RsLane& c, unsigned char* wbuf,
+                                         const unsigned char* smem, int lane, int f, double theta_s, double W,
+                                         double& mx, bool& amb, bool& nanf) {
+    double2* buf = reinterpret_cast<double2*>(wbuf + RS_BUF);
+    double2 x[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int q = t * HOP - NFFT / 2 + 2 * (lane + 64 * r);
+        x[r] = make_double2(c.win[2 * r] * (double)seg_sample(v, q), c.win[2 * r + 1] * (double)seg_sample(v, q + 1));
+    }
+    // radix-4 Stockham autosort: v[r] = d[j + 64 r], v[r] *= W_{4 Ns}^{r (j % Ns)}, DFT4,
+    // V[r] -> d'[(j / Ns) 4 Ns + j % Ns + r Ns]; natural order after Ns = 64
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        if (it > 0) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) x[r] = buf[lane + 64 * r];
+#pragma unroll
+            for (int r = 1; r < 4; ++r) x[r] = zmul(x[r], c.tw[3 * (it - 1) + r - 1]);
+        }
+        const double2 a0 = make_double2(x[0].x + x[2].x, x[0].y + x[2].y);
+        const double2 a1 = make_double2(x[0].x - x[2].x, x[0].y - x[2].y);
+        const double2 a2 = make_double2(x[1].x + x[3].x, x[1].y + x[3].y);
+        const double2 a3 = make_double2(x[1].x - x[3].x, x[1].y - x[3].y);
+        x[0] = make_double2(a0.x + a2.x, a0.y + a2.y);
+        x[2] = make_double2(a0.x - a2.x, a0.y - a2.y);
+        x[1] = make_double2(a1.x + a3.y, a1.y - a3.x);   // a1 - i a3
+        x[3] = make_double2(a1.x - a3.y, a1.y + a3.x);   // a1 + i a3
+        const int lg = 2 * it;
+        const int base = it < 3 ? ((lane >> lg) << (lg + 2)) + (lane & ((1 << lg) - 1)) : lane;
+        wave_sync();   // every lane has read this iteration's inputs
+#pragma unroll
+        for (int r = 0; r < 4; ++r) buf[base + (r << lg)] = x[r];   // (it = 3: Z[lane + 64 r])
+        wave_sync();
+    }
+    // untangle: X[k] = E + W512^k O,  E = (Z[k] + conj Z[256-k]) / 2,  O = (Z[k] - conj Z[256-k]) / 2i
+    double p[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int k = lane + 64 * r;
+        const double2 zk = x[r], zc = buf[(256 - k) & 255];
+        const double er = 0.5 * (zk.x + zc.x), ei = 0.5 * (zk.y - zc.y);
+        const double orr = 0.5 * (zk.y + zc.y), oi = -0.5 * (zk.x - zc.x);
+        const double2 cs = c.tu[r];
+        const double xr = er + (orr * cs.x + oi * cs.y);
+        const double xi = ei + (oi * cs.x - orr * cs.y);
+        p[r] = xr * xr + xi * xi;
+    }
+    const double d256 = x[0].x - x[0].y;   // k = 256 (lane 0): W512^256 = -1 exactly
+    wave_sync();
+    double* P = reinterpret_cast<double*>(buf);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) P[lane + 64 * r] = p[r];
+    if (lane == 0) P[256] = d256 * d256;
+    wave_sync();
+    // mel (every non-zero weight of the band, in bin order) + dB; lane: bands lane, 127 - lane
+    const int* mlo = reinterpret_cast<const int*>(smem + RS_MLO);
+    const int* moff = reinterpret_cast<const int*>(smem + RS_MOFF);
+    const float* mw = reinterpret_cast<const float*>(smem + RS_MW);
+    double* xa = reinterpret_cast<double*>(wbuf + RS_XA);
+    float* xb = reinterpret_cast<float*>(wbuf + RS_XB);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int m = h ? NMEL - 1 - lane : lane;
+        const int lo = mlo[m], o0 = moff[m], o1 = moff[m + 1];
+        double acc = 0.0;
+        for (int o = o0; o < o1; ++o) acc = fma((double)mw[o], P[lo + o - o0], acc);
+        const double db = 10.0 * log10(acc < 1e-10 ? 1e-10 : acc);   // np.maximum: NaN propagates
+        const bool keep = db >= theta_s;
+        xa[m * kRsFrames + f] = keep ? db : 0.0;
+        xb[m * kRsFrames + f] = keep ? 0.0f : 1.0f;
+        mx = fmax(mx, db);
+        amb = amb || fabs(db - theta_s) <= W;
+        nanf = nanf || db != db;
+    }
+    wave_sync();
+}
+
+// DCT of the chunk's n frames split at theta_s: lane k < 20 returns A_k, B_k of frames 0..7.
+// Lanes (k, h) = (l % 20, l / 20), l < 60, take bands [43 h, 43 h + 43); the thirds are
+// added in a fixed order (h = 0, 1, 2).
+__device__ __forceinline__ void rs_dct(const unsigned char* smem, unsigned char* wbuf, int lane, double (&A)[8],
+                                       double (&B)[8]) {
+    const double* D = reinterpret_cast<const double*>(smem + RS_D);
+    double* xa = reinterpret_cast<double*>(wbuf + RS_XA);
+    const float* xb = reinterpret_cast<const float*>(wbuf + RS_XB);
+#pragma unroll
+    for (int f = 0; f < 8; ++f) { A[f] = 0.0; B[f] = 0.0; }
+    if (lane < 60) {
+        const int k = lane % NMFCC, h = lane / NMFCC;
+        const int m0 = 43 * h, m1 = min(NMEL, m0 + 43);
+        for (int m = m0; m < m1; ++m) {
+            const double d = D[m * NMFCC + k];
+            const double4* pa = reinterpret_cast<const double4*>(xa + m * kRsFrames);
+            const float4* pb = reinterpret_cast<const float4*>(xb + m * kRsFrames);
+            const double4 a0 = pa[0], a1 = pa[1];
+            const float4 b0 = pb[0], b1 = pb[1];
+            const double av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+            const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+            for (int f = 0; f < 8; ++f) {
+                A[f] = fma(d, av[f], A[f]);
+                B[f] = fma(d, (double)bv[f], B[f]);
+            }
+        }
+    }
+    wave_sync();
+    if (lane >= NMFCC && lane < 60) {   // thirds 1, 2 park their sums in the (consumed) XA tile
+        double* red = xa + (lane - NMFCC) * 16;
+#pragma unroll
+        for (int f = 0; f < 8; ++f) { red[f] = A[f]; red[8 + f] = B[f]; }
+    }
+    wave_sync();
+    if (lane < NMFCC) {
+        const double* r1 = xa + lane * 16;
+        const double* r2 = xa + (NMFCC + lane) * 16;
+#pragma unroll
+        for (int f = 0; f < 8; ++f) {
+            A[f] = (A[f] + r1[f]) + r2[f];
+            B[f] = (B[f] + r1[8 + f]) + r2[8 + f];
+        }
+    }
+    wave_sync();
+}
+
+__device__ __forceinline__ double wave_max_d(double x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = fmax(x, __shfl_xor(x, o, 64));
+    return x;
+}
+
+// One chunk (frames 8c .. 8c + n - 1): lane k < 20 returns its 7 sums {rA, rB, sA, sB, sAA,
+// sAB, sBB} (shift = the chunk's first frame); mx / n / flags are wave-uniform.
+__device__ void rs_chunk(const SegView& v, int T, int c, double theta_s, double W, const RsLane& cl,
+                         const unsigned char* smem, unsigned char* wbuf, int lane, double (&pv)[7], double& mx,
+                         int& n, int& flags) {
+    const int t0 = c * kRsFrames;
+    n = min(kRsFrames, T - t0);
+    double m = -INFINITY;
+    bool amb = false, nanf = false;
+    for (int f = 0; f < n; ++f) rs_frame(v, t0 + f, cl, wbuf, smem, lane, f, theta_s, W, m, amb, nanf);
+    double A[8], B[8];
+    rs_dct(smem, wbuf, lane, A, B);
+    const double rA = A[0], rB = B[0];
+    double sA = 0.0, sB = 0.0, sAA = 0.0, sAB = 0.0, sBB = 0.0;
+#pragma unroll
+    for (int f = 1; f < 8; ++f) {
+        if (f < n) {
+            const double dA = A[f] - rA, dB = B[f] - rB;
+            sA += dA;
+            sB += dB;
+            sAA = fma(dA, dA, sAA);
+            sAB = fma(dA, dB, sAB);
+            sBB = fma(dB, dB, sBB);
+        }
+    }
+    pv[0] = rA; pv[1] = rB; pv[2] = sA; pv[3] = sB; pv[4] = sAA; pv[5] = sAB; pv[6] = sBB;
+    mx = wave_max_d(m);
+    flags = (__ballot(amb) ? 1 : 0) | (__ballot(nanf) ? 2 : 0);
+}
+
+// Chunk sums merged in chunk order as polynomials in theta (the clamp is known only at the end):
+// S1(theta) = P1a + theta P1b, S2(theta) = P2a + theta P2b + theta^2 P2c around the first
+// chunk's first frame c_0(theta) = rA0 + theta rB0.
+struct RsAcc {
+    double rA0 = 0.0, rB0 = 0.0, P1a = 0.0, P1b = 0.0, P2a = 0.0, P2b = 0.0, P2c = 0.0;
+    bool init = false;
+};
+
+__device__ __forceinline__ void rs_merge(RsAcc& s, const double (&pv)[7], int n) {
+    const double rA = pv[0], rB = pv[1], sA = pv[2], sB = pv[3], sAA = pv[4], sAB = pv[5], sBB = pv[6];
+    if (!s.init) {
+        s.rA0 = rA; s.rB0 = rB;
+        s.P1a = sA; s.P1b = sB;
+        s.P2a = sAA; s.P2b = 2.0 * sAB; s.P2c = sBB;
+        s.init = true;
+        return;
+    }
+    const double dA = rA - s.rA0, dB = rB - s.rB0, nd = (double)n;
+    s.P2a += sAA + 2.0 * dA * sA + nd * dA * dA;
+    s.P2b += 2.0 * sAB + 2.0 * dA * sB + 2.0 * dB * sA + 2.0 * nd * dA * dB;
+    s.P2c += sBB + 2.0 * dB * sB + nd * dB * dB;
+    s.P1a += sA + nd * dA;
+    s.P1b += sB + nd * dB;
+}
+
+// Finish one slot (one wave): the exact theta from the chunk maxima, the ambiguous chunks
+// recomputed with it, the merge, mean / population std, the reference's float64 (or float32)
+// score arithmetic and the outputs.  parts == nullptr: serial slot (every chunk computed here).
+template <int RING>
+__device__ void rs_finish(const RsArgs& a, RsSlot* sp, int seg, int T, float theta_s32, const RsPart* parts,
+                          const RsLane& cl, const unsigned char* smem, unsigned char* wbuf, int lane) {
+    const SegView v = rs_view<RING>(a, seg);
+    const int nch = (T + kRsFrames - 1) / kRsFrames;
+    const double theta_s = (double)theta_s32;
+    double mx = -INFINITY;
+    int fl = 0;
+    RsAcc acc;
+    double pv[7];
+    if (parts) {
+        for (int c = 0; c < nch; ++c) {
+            mx = fmax(mx, parts[c].mx);
+            fl |= parts[c].flags;
+        }
+    } else {   // serial: a first pass with theta_s, merged as it goes
+        for (int c = 0; c < nch; ++c) {
+            double m;
+            int n, f;
+            rs_chunk(v, T, c, theta_s, kRsWindow, cl, smem, wbuf, lane, pv, m, n, f);
+            mx = fmax(mx, m);
+            fl |= f;
+            rs_merge(acc, pv, n);
+        }
+    }
+    const double theta = mx - kRsTopDb;
+    const bool nan_in = (fl & 2) != 0;
+    const bool redo_all = !(fabs(theta - theta_s) <= kRsWindow);
+    if (!nan_in && (parts || redo_all || (fl & 1))) {
+        if (!parts) acc = RsAcc();
+        for (int c = 0; c < nch; ++c) {
+            int n;
+            if (!parts || redo_all || (parts[c].flags & 1)) {   // classification at the exact theta
+                double m;
+                int f;
+                rs_chunk(v, T, c, theta, -1.0, cl, smem, wbuf, lane, pv, m, n, f);
+            } else {
+                n = parts[c].n;
+                if (lane < NMFCC) {
+#pragma unroll
+                    for (int q = 0; q < 7; ++q) pv[q] = parts[c].v[q * NMFCC + lane];
+                }
+            }
+            rs_merge(acc, pv, n);
+        }
+    }
+    double mean = 0.0, sd = 0.0;
+    if (lane < NMFCC) {
+        const double Td = (double)T;
+        const double S1 = fma(theta, acc.P1b, acc.P1a);
+        const double S2 = acc.P2a + theta * acc.P2b + theta * theta * acc.P2c;
+        mean = fma(theta, acc.rB0, acc.rA0) + S1 / Td;
+        double var = (S2 - S1 * S1 / Td) / Td;
+        sd = sqrt(var > 0.0 ? var : 0.0);
+        if (nan_in) { mean = __builtin_nan(""); sd = __builtin_nan(""); }
+        if (a.out_mean64) {
+            a.out_mean64[(int64_t)seg * NMFCC + lane] = mean;
+            a.out_std64[(int64_t)seg * NMFCC + lane] = sd;
+        }
+    }
+    double* st = reinterpret_cast<double*>(wbuf + RS_BUF);
+    if (lane < NMFCC) { st[lane] = mean; st[NMFCC + lane] = sd; }
+    wave_sync();
+    if (lane == 0) {
+        if (a.has_template) {
+            double score;
+            if (a.cand_f32) {
+                float c32[2 * NMFCC];
+                for (int i = 0; i < 2 * NMFCC; ++i) c32[i] = (float)st[i];
+                score = score_f32cand(a.tmpl, a.tmpl + NMFCC, c32, c32 + NMFCC);
+            } else {
+                score = score_f64cand(a.tmpl, a.tmpl + NMFCC, st, st + NMFCC);
+            }
+            const int match = score >= a.threshold;
+            if (RING) {
+                a.events[seg].score = score;
+                a.events[seg].match = match;
+                a.events[seg].flags |= EWK_EV_RESCORED;
+            } else {
+                if (a.out_score) a.out_score[seg] = score;
+                if (a.out_match) a.out_match[seg] = (uint8_t)match;
+            }
+        }
+        __hip_atomic_store(&sp->nclaim, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // finished
+    }
+    wave_sync();
+}
+
+// List segment `seg` (lane 0 of its scoring wave, after its float32 score is written).
+__device__ __forceinline__ void rs_list(const ScoreArgs& a, int seg, int len, float theta_s) {
+    const int s = atomicAdd(&a.rs_ctl[0], 1);
+    if (s >= a.rs_cap) return;   // list full: the float32 score stands
+    const int T = 1 + len / HOP;
+    const int nch = (T + kRsFrames - 1) / kRsFrames;
+    int serial = a.list_all, base = 0;   // list_all (every segment): one wave each, no part records
+    if (!serial) {
+        base = atomicAdd(&a.rs_ctl[1], nch);
+        if (base > a.rs_part_cap - nch) serial = 1;   // part pool full: this slot runs serially
+    }
+    RsSlot* p = a.rs_slots + s;
+    p->seg = seg;
+    p->T = T;
+    p->base = base;
+    p->cursor = 0;
+    p->done = 0;
+    p->theta_s = theta_s;
+    p->serial = serial;
+    __hip_atomic_store(&p->nclaim, serial ? 1 : nch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Lane 0: claim the next unit (a chunk, or a whole serial slot).  nclaim: 0 not yet published,
+// -1 finished, > 0 claimable units.  The scan hint moves past a prefix of slots whose units are
+// all taken.
+struct RsClaim {
+    int slot = -1, unit = 0, seg = 0, T = 0, base = 0, serial = 0, nclaim = 0;
+    float theta_s = 0.0f;
+};
+__device__ __forceinline__ RsClaim rs_claim(const RsArgs& a) {
+    RsClaim r;
+    const int n = min(__hip_atomic_load(&a.rs_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.rs_cap);
+    bool prefix = true;
+    for (int s = __hip_atomic_load(&a.rs_ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); s < n; ++s) {
+        RsSlot* p = a.rs_slots + s;
+        const int nc = __hip_atomic_load(&p->nclaim, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if (nc == 0) { prefix = false; continue; }
+        if (nc > 0) {
+            const int u = __hip_atomic_fetch_add(&p->cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (u < nc) {
+                r.slot = s; r.unit = u; r.nclaim = nc;
+                r.seg = p->seg; r.T = p->T; r.base = p->base; r.serial = p->serial; r.theta_s = p->theta_s;
+                return r;
+            }
+        }
+        if (prefix) __hip_atomic_fetch_max(&a.rs_ctl[2], s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return r;
+}
+
+// One wave drains the list until nothing is claimable; true if it finished a slot.
+template <int RING>
+__device__ __attribute__((noinline)) bool rs_drain(const RsArgs& a, unsigned char* smem, int wave, int lane) {
+    unsigned char* wbuf = smem + RS_WAVES + wave * RS_WAVE_BYTES;
+    RsLane cl;
+    bool have_lane = false, finished = false;
+    for (;;) {
+        RsClaim c;
+        if (lane == 0) c = rs_claim(a);
+        const int slot = __shfl(c.slot, 0, 64);
+        if (slot < 0) break;
+        const int unit = __shfl(c.unit, 0, 64), seg = __shfl(c.seg, 0, 64), T = __shfl(c.T, 0, 64);
+        const int base = __shfl(c.base, 0, 64), serial = __shfl(c.serial, 0, 64), nclaim = __shfl(c.nclaim, 0, 64);
+        const float theta_s = __shfl(c.theta_s, 0, 64);
+        if (!have_lane) { rs_lane_init(a.tab64, lane, cl); have_lane = true; }
+        RsSlot* sp = a.rs_slots + slot;
+        if (serial) {
+            rs_finish<RING>(a, sp, seg, T, theta_s, nullptr, cl, smem, wbuf, lane);
+            finished = true;
+            continue;
+        }
+        const SegView v = rs_view<RING>(a, seg);
+        double pv[7], mx;
+        int n, flags;
+        rs_chunk(v, T, unit, (double)theta_s, kRsWindow, cl, smem, wbuf, lane, pv, mx, n, flags);
+        RsPart* pp = a.rs_parts + base + unit;
+        if (lane < NMFCC) {
+#pragma unroll
+            for (int q = 0; q < 7; ++q) pp->v[q * NMFCC + lane] = pv[q];
+        }
+        if (lane == 0) { pp->mx = mx; pp->n = n; pp->flags = flags; }
+        __threadfence();   // the part record before the count (release)
+        int last = 0;
+        if (lane == 0) last = __hip_atomic_fetch_add(&sp->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nclaim - 1;
+        if (__shfl(last, 0, 64)) {
+            __threadfence();   // every part record of the slot (acquire)
+            rs_finish<RING>(a, sp, seg, T, theta_s, a.rs_parts + base, cl, smem, wbuf, lane);
+            finished = true;
+        }
+    }
+    return finished;
+}
+
+// Anything listed that no wave has taken yet (thread 0)?
+__device__ __forceinline__ bool rs_pending(const RsArgs& a) {
+    const int n = min(__hip_atomic_load(&a.rs_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.rs_cap);
+    return n > __hip_atomic_load(&a.rs_ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// End of every k_score_f32 workgroup (all modes), after its float32 work: drain the re-score
+// list, count out; the last workgroup out drains the rest, resets the counters for the next
+// launch (ring mode: advances the event watermark) and writes the poll mirror.  Writers
+// publish with a device-scope release before their arrival count: only a workgroup that wrote
+// something the last one reads (a listed segment, a finished slot, or -- with a poll mirror --
+// any score) pays it.  `listed`: lane 0 of a wave that did.
+template <int RING>
+__device__ void score_tail(const ScoreArgs& a, unsigned char* smem, bool listed) {
+    int* flag = reinterpret_cast<int*>(smem + L_WG);   // [0] last, [1 + wave] listed, [1 + WAVES] pending
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const RsArgs ra = rs_args(a);
+    bool loaded = false;
+    __syncthreads();   // every wave is done with the float32 tables and scratch
+    if (a.rs_slots) {
+        if (threadIdx.x == 0) flag[1 + WAVES] = rs_pending(ra);
+        __syncthreads();
+        if (flag[1 + WAVES]) {
+            rs_load_tables(a.tab64, smem);
+            __syncthreads();
+            loaded = true;
+            listed = rs_drain<RING>(ra, smem, wave, lane) || listed;
+        }
+    }
+    if (lane == 0) flag[1 + wave] = listed;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int any = 0;
+        for (int w = 0; w < WAVES; ++w) any |= flag[1 + w];
+        if (any) __threadfence();
+        flag[0] = __hip_atomic_fetch_add(&a.rs_ctl[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                  (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    __threadfence();   // acquire what every other workgroup released before its count
+    if (a.rs_slots) {   // the last workgroup: every other has drained and counted out
+        if (threadIdx.x == 0) flag[1 + WAVES] = rs_pending(ra);
+        __syncthreads();
+        if (flag[1 + WAVES]) {
+            if (!loaded) {
+                rs_load_tables(a.tab64, smem);
+                __syncthreads();
+            }
+            rs_drain<RING>(ra, smem, wave, lane);
+        }
+        __syncthreads();
+        // finished slots (-1) back to "not published" for the next launch
+        const int n = min(__hip_atomic_load(&a.rs_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.rs_cap);
+        for (int i = threadIdx.x; i < n; i += blockDim.x) a.rs_slots[i].nclaim = 0;
+    }
+    if (threadIdx.x == 0) {
+        if (RING) *a.adv_ev_base = *a.n_events;
+        *a.work = 0;
+        a.rs_ctl[0] = 0;
+        a.rs_ctl[1] = 0;
+        a.rs_ctl[2] = 0;
+        a.rs_ctl[3] = 0;
+        __threadfence();
+    }
+    if (RING && a.mirror) {   // poll mirror: the bank's counters and first events -> pinned host memory
+        __syncthreads();   // this workgroup's re-score writes are done and fenced by thread 0
+        const volatile int32_t* vc = a.evc;
+        const uint4 c = make_uint4((uint32_t)vc[0], (uint32_t)vc[1], (uint32_t)vc[2], (uint32_t)vc[3]);
+        const int32_t n = (int32_t)min(min((uint32_t)(c.x - (uint32_t)a.ev_base0), (uint32_t)a.n_seg),
+                                       (uint32_t)a.mirror_chunk);
+        if (threadIdx.x == 0) *reinterpret_cast<uint4*>(a.mirror) = c;
+        const uint4* src = reinterpret_cast<const uint4*>(a.events);
+        uint4* dst = reinterpret_cast<uint4*>(a.mirror + 16);
+        const int nq = n * (int)(sizeof(ewk_event) / 16);
+        // every workgroup that wrote a score released it before its arrival count, and the
+        // fence above (after the last arrival) acquired them for this workgroup
+        for (int i = threadIdx.x; i < nq; i += blockDim.x) dst[i] = src[i];
+    }
+}
