@@ -77,7 +77,14 @@ def parse():
     ap.add_argument("--big-ticks", type=int, default=300, help="ticks after the prefill for the big runs")
     ap.add_argument("--fixed-len", type=int, default=16000,
                     help="also time the scorer on segments of this one length (0 = skip)")
+    ap.add_argument("--short-len", type=int, default=6400,
+                    help="also time the scorer on segments of this length (short_length; 0 = skip)")
     ap.add_argument("--confirm-batch", type=int, default=64, help="config 5: Whisper-tiny batch (0 = skip)")
+    ap.add_argument("--no-host-ingest", dest="host_ingest", action="store_false",
+                    help="skip the pinned-host ingest legs (streaming_host_ingest)")
+    ap.add_argument("--host-streams-f32", type=int, default=131072)
+    ap.add_argument("--host-streams-i16", type=int, default=1048576)
+    ap.add_argument("--host-ticks", type=int, default=200, help="timed ticks of the host-ingest legs")
     return ap.parse_args()
 
 
@@ -133,8 +140,32 @@ def make_segments(torch, dev, n_seg, seed, word, fixed_len=0):
 
 
 # --------------------------------------------------------------------------- CPU baseline
+def _pin(cpu):
+    """Pin this worker process to one host CPU (None: leave it floating)."""
+    if cpu is not None:
+        try:
+            os.sched_setaffinity(0, {int(cpu)})
+        except (AttributeError, OSError):
+            pass
+
+
+def worker_cpus(procs):
+    """One distinct CPU per worker, spread over this process's affinity mask (a GPU box may
+    list 256 host CPUs for a 16-core quota: unpinned workers migrate and time-share, which
+    made round 3's per-process rates spread 231 %)."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        return [None] * procs
+    if len(cpus) < procs:
+        return [None] * procs
+    step = len(cpus) // procs
+    return [cpus[i * step] for i in range(procs)]
+
+
 def _cpu_worker(args):
-    seg_list, seconds = args
+    seg_list, seconds, cpu = args
+    _pin(cpu)
     os.environ["OMP_NUM_THREADS"] = "1"
     from oracle import mfcc_ref
     tm, ts = mfcc_ref.extract_mfcc(load_word())
@@ -175,20 +206,23 @@ def cpu_baseline(host_pcm, lengths, offsets, seconds):
     import multiprocessing as mp
     procs, aff, quota = host_cores()
     per = max(1, len(lengths) // procs)
+    cpus = worker_cpus(procs)
     jobs = []
     for p in range(procs):
         idx = range(p * per, min(len(lengths), (p + 1) * per))
         jobs.append(([host_pcm[offsets[i] - offsets[0]: offsets[i] - offsets[0] + lengths[i]] for i in idx],
-                     seconds))
+                     seconds, cpus[p]))
     ctx = mp.get_context("spawn")
     with ctx.Pool(procs, initializer=_pool_init) as pool:
-        res = pool.map(_cpu_worker, jobs)
+        res = pool.map(_cpu_worker, jobs, chunksize=1)
     frames = sum(r[0] for r in res)
     segs = sum(r[1] for r in res)
     wall = max(r[2] for r in res)
     rates = np.array([r[0] / r[2] for r in res if r[2] > 0])   # each worker process's own rate
     return {"value": frames / wall, "unit": "frames/s", "cores": procs, "host_cores_affinity": aff,
-            "cpu_quota_cores": quota, "kind": "port",
+            "cpu_quota_cores": quota, "kind": "port", "pinned": cpus[0] is not None,
+            # robust to one slow or one unusually idle core: the median process rate x cores
+            "median_x_cores": float(np.median(rates) * procs),
             # per-core rate and its spread over the worker processes: the aggregate depends on
             # how many cores the box's cgroup grants and how busy its other tenants keep them
             "per_core": {"median": float(np.median(rates)), "min": float(rates.min()), "max": float(rates.max()),
@@ -221,7 +255,8 @@ def event_kind(rng, n):
 def _cpu_stream_worker(args):
     """Faithful CPU level 1 + level 2 (oracle/gate_ref.py DetectorRef + mfcc_ref scoring of every
     emitted segment) on one synthetic stream of the streaming bench's recipe, ~`seconds` of work."""
-    seed, seconds = args
+    seed, seconds, cpu = args
+    _pin(cpu)
     os.environ["OMP_NUM_THREADS"] = "1"
     from oracle import gate_ref, mfcc_ref
     word = load_word()
@@ -252,10 +287,12 @@ def cpu_stream_baseline(seconds, procs):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
     with ctx.Pool(procs, initializer=_pool_init) as pool:
-        res = pool.map(_cpu_stream_worker, [(9000 + p, seconds) for p in range(procs)])
+        cpus = worker_cpus(procs)
+        res = pool.map(_cpu_stream_worker, [(9000 + p, seconds, cpus[p]) for p in range(procs)], chunksize=1)
     rtf = sum(t * 0.1 / w for t, w in res)       # seconds of audio per second, summed over processes
     per = np.array([t * 0.1 / w for t, w in res])
     return {"value": rtf, "unit": "streams sustained in real time", "cores": procs, "kind": "port",
+            "pinned": cpus[0] is not None, "median_x_cores": float(np.median(per) * procs),
             "per_core": {"median": float(np.median(per)), "min": float(per.min()), "max": float(per.max()),
                          "spread_pct": float(100.0 * (per.max() - per.min()) / np.median(per)),
                          "unit": "real-time streams per process"},
@@ -266,6 +303,7 @@ def cpu_stream_baseline(seconds, procs):
 
 def _pool_init():
     os.environ["OMP_NUM_THREADS"] = "1"
+    os.environ["OPENBLAS_NUM_THREADS"] = "1"
     sys.path.insert(0, ROOT)
 
 
@@ -300,7 +338,7 @@ def confirm_bench(se, ev, final_tick, batch, dev):
 
 
 def fixed_length_bench(torch, dev, ewa, eng, word, n_seg, seed, sh, fixed_len=16000, reps=5):
-    """Scorer kernel on n_seg segments of one fixed length (L = 16000, T = 101 frames each)."""
+    """Scorer kernel on n_seg segments of one fixed length (default L = 16000, T = 101 frames each)."""
     pcm, d_off, d_len, frames, _, _ = make_segments(torch, dev, n_seg, seed + 17, word, fixed_len=fixed_len)
     mean = torch.empty((n_seg, 20), device=dev, dtype=torch.float32)
     std = torch.empty((n_seg, 20), device=dev, dtype=torch.float32)
@@ -512,6 +550,92 @@ def streaming_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, world=1
     return out
 
 
+def streaming_host_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, ring_samples=0, pcm16=False,
+                         prefill=100):
+    """End-to-end ingest: every tick's PCM of all `n_streams` streams starts in PINNED HOST
+    memory (what a capture server holds after its sockets / sound cards deliver a block per
+    stream), is DMA'd to the GPU over PCIe on a copy stream (double-buffered device staging,
+    tick t+1's copy overlapping tick t's gate and scorer), then pushed (the reference's
+    callback ingest, wakeword.py:438-444, 454-470).  Input: make_shifted_signal, so tick t of
+    all streams is ONE contiguous host slice of n_streams x 1600 samples and every tick moves
+    n_streams x 6.4 KB (3.2 KB int16) over PCIe -- the real per-tick volume."""
+    sig = make_shifted_signal(torch, dev, n_streams, prefill + n_ticks + 1, seed, word, pcm16=pcm16)
+    host = torch.empty(sig.numel(), dtype=sig.dtype, pin_memory=True)
+    host.copy_(sig)
+    del sig
+    torch.cuda.empty_cache()
+    es = 2 if pcm16 else 4
+    se = eng_mod.StreamEngine(n_streams, gpu=dev.index if dev.index is not None else 0,
+                              ring_samples=int(ring_samples), ring_format=1 if pcm16 else 0)
+    push = se.push_device_pcm16 if pcm16 else se.push_device
+    se.template_from_pcm(word)
+    per = n_streams * 1600
+    stage = [torch.empty(per, dtype=host.dtype, device=dev) for _ in range(2)]
+    cs = torch.cuda.Stream(dev)
+    es_ = torch.cuda.ExternalStream(se.stream_handle(), device=dev)
+    copied = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    c_start = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    free = [torch.cuda.Event() for _ in range(2)]
+    free_used = [False, False]
+    copy_ms = []
+
+    def copy(t):
+        b = t % 2
+        with torch.cuda.stream(cs):
+            if free_used[b]:
+                cs.wait_event(free[b])          # the gate of tick t-2 has read this staging buffer
+            c_start[b].record(cs)
+            stage[b].copy_(host[t * 1600: t * 1600 + per], non_blocking=True)
+            copied[b].record(cs)
+
+    events = []
+
+    def run(t0, nt, timed):
+        copy(t0)
+        for t in range(t0, t0 + nt):
+            b = t % 2
+            if t + 1 < t0 + nt:
+                copy(t + 1)                     # the next tick's DMA, ahead of this tick's kernels
+            es_.wait_event(copied[b])
+            push(stage[b].data_ptr(), 1600, 0, 1)
+            free[b].record(es_)
+            free_used[b] = True
+            events.append(se.poll(lagged=True))
+            if timed and t > t0:                # the previous copy has surely finished by now
+                pb = (t - 1) % 2
+                copied[pb].synchronize()
+                copy_ms.append(c_start[pb].elapsed_time(copied[pb]))
+        events.append(se.poll())
+
+    run(0, prefill, False)
+    se.sync()
+    torch.cuda.synchronize()
+    events.clear()
+    w0 = time.perf_counter()
+    run(prefill, n_ticks, True)
+    se.sync()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - w0
+    ev = np.concatenate(events)
+    real = ev[(ev["flags"] & 1) == 0]
+    per_tick = wall / n_ticks
+    h2d = float(np.median(copy_ms)) if copy_ms else None
+    out = {"streams": n_streams, "resident": False, "ingest": "pinned host -> HBM DMA every tick (copy stream, "
+                                                            "double-buffered), then push",
+           "ticks": n_ticks, "ring_format": "int16" if pcm16 else "float32",
+           "ring_samples_per_stream": int(ring_samples) or 10 * SR,
+           "h2d_bytes_per_tick": per * es, "h2d_ms_per_tick_median": h2d,
+           "h2d_gbs": per * es / (h2d / 1e3) / 1e9 if h2d else None,
+           "wall_s": wall, "ms_per_tick": per_tick * 1e3, "realtime": per_tick <= 0.1,
+           "realtime_headroom": 0.1 / per_tick,
+           "streams_realtime": n_streams * min(1.0, 0.1 / per_tick),
+           "events": int(len(real)), "matches": int(real["match"].sum()) if len(real) else 0}
+    se.close()
+    del host, stage
+    torch.cuda.empty_cache()
+    return out
+
+
 def _rccl_version(torch):
     try:
         v = torch.cuda.nccl.version()
@@ -616,6 +740,10 @@ def main():
 
     fixed = fixed_length_bench(torch, dev, ewa, eng, word, n_seg, args.seed + 1000 * rank, sh) \
         if args.fixed_len > 0 and world == 1 else None
+    # the reference's shortest gated segment (0.4 s: speech_duration_min 0.3 s + padding), where
+    # the per-segment fixed cost weighs most
+    short = fixed_length_bench(torch, dev, ewa, eng, word, n_seg, args.seed + 1000 * rank, sh,
+                               fixed_len=args.short_len) if args.short_len > 0 and world == 1 else None
     kernel_s = (k_ms / max(1, k_n)) / 1e3
     achieved = frames * BYTES_PER_FRAME / kernel_s / 1e9
     traffic, traffic_src, compute = None, None, None
@@ -680,6 +808,8 @@ def main():
     }
     if fixed is not None:
         out["fixed_length"] = fixed
+    if short is not None:
+        out["short_length"] = short
     if world > 1:   # what the collectives actually ran on (a SCALE run can check RCCL saw N ranks)
         out["distributed"] = {"world_size_seen": dist.get_world_size(), "backend": str(dist.get_backend()),
                               "rccl_version": _rccl_version(torch), "positives_gathered_to_rank0": gathered[0],
@@ -714,6 +844,21 @@ def main():
             r["requested_streams"] = n_req
             out[key] = r
             best = max(best, r["streams_realtime"])
+        if args.host_ingest and world == 1:
+            # end-to-end ingest from pinned host memory (the resident legs above start with the
+            # audio already in HBM): the reference's 10 s float32 rings, and 3 s int16 rings
+            hi = {}
+            for key, n_req, ring, p16 in (("f32_131072", args.host_streams_f32, 0, False),
+                                          ("i16_1048576", args.host_streams_i16, args.max_ring, True)):
+                if n_req <= 0:
+                    continue
+                torch.cuda.empty_cache()
+                n = min(n_req, fit_streams(torch, dev, ring or 10 * SR, 0, sample_bytes=2 if p16 else 4))
+                hi[key] = streaming_host_bench(torch, dev, ewa, n, args.host_ticks, args.seed + 47, word,
+                                               ring_samples=ring, pcm16=p16)
+                hi[key]["requested_streams"] = n_req
+            out["streaming_host_ingest"] = hi
+            out["streams_realtime_host_ingest"] = max([r["streams_realtime"] for r in hi.values()] or [0.0])
         tot = torch.tensor([best], dtype=torch.float64, device=cdev)
         if world > 1:
             dist.all_reduce(tot)

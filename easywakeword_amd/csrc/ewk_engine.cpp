@@ -571,9 +571,13 @@ static int score_linear(ewk_engine* e, const float* d_pcm, const int64_t* d_off,
     a.out_std = d_std;
     a.out_score = d_score;
     a.out_match = d_match;
-    {   // (launch_score_f32 zeroes the work and re-score counters; the fp64 re-score runs inside)
+    {   // (launch_score_f32 zeroes the work and re-score counters)
         ProfScope ps(e, 0, s);
         HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));
+    }
+    {
+        ProfScope ps(e, 1, s);
+        HIP_TRY(launch_rescore_linear(a, s));
     }
     return EWK_OK;
 }
@@ -645,6 +649,7 @@ int ewk_score_segments(ewk_engine* e, const float* pcm, int64_t n_pcm, const int
         a.out_match = e->match.p;
         a.cand_f32 = (flags & EWK_SCORE_F32_CANDIDATES) ? 1 : 0;
         HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));   // (zeroes the work and re-score counters)
+        HIP_TRY(launch_rescore_linear(a, s));
     }
     if (out_mean) HIP_TRY(hipMemcpyAsync(out_mean, e->mean.p, (size_t)n_seg * NMFCC * 4, hipMemcpyDeviceToHost, s));
     if (out_std) HIP_TRY(hipMemcpyAsync(out_std, e->stdv.p, (size_t)n_seg * NMFCC * 4, hipMemcpyDeviceToHost, s));
@@ -693,6 +698,7 @@ int ewk_score_segments_f64(ewk_engine* e, const float* pcm, int64_t n_pcm, const
     a.out_mean64 = e->mean64.p;
     a.out_std64 = e->std64.p;
     HIP_TRY(launch_score_f32(e->d_tab, a, 0, s));
+    HIP_TRY(launch_rescore_linear(a, s));
     if (out_mean) HIP_TRY(hipMemcpyAsync(out_mean, e->mean64.p, (size_t)n_seg * NMFCC * 8, hipMemcpyDeviceToHost, s));
     if (out_std) HIP_TRY(hipMemcpyAsync(out_std, e->std64.p, (size_t)n_seg * NMFCC * 8, hipMemcpyDeviceToHost, s));
     if (out_score && e->has_tmpl)

@@ -1067,7 +1067,14 @@ __device__ __forceinline__ void scout_batch(const SegSrc<RING>& v, int t0, int l
 template <int RING>
 __device__ __forceinline__ float scout_tiles(const SegSrc<RING>& v, int ntile, int lane) {
     float e = -1.0f;
-    for (int t0 = 0; t0 < ntile; t0 += kScoutBatch) scout_batch<RING, kScoutBatch>(v, t0, lane, e);
+    for (int t0 = 0; t0 < ntile; t0 += kScoutBatch) {
+        // the batch sized to the tiles left (a short segment's scout issues 2 or 4 tiles' loads
+        // and reductions, not 8)
+        const int left = ntile - t0;
+        if (left <= 2) scout_batch<RING, 2>(v, t0, lane, e);
+        else if (left <= 4) scout_batch<RING, 4>(v, t0, lane, e);
+        else scout_batch<RING, kScoutBatch>(v, t0, lane, e);
+    }
     return e;
 }
 
@@ -1567,7 +1574,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
         // one segment per workgroup: a workgroup without one skips the table fill (most of
         // a quiet tick's 256 workgroups)
         if (MODE == 1 && (int)blockIdx.x >= r_count) {
-            score_tail<RING>(a, smem, false);
+            score_tail<RING>(a, smem, false, false);   // nothing can be listed yet: count out at once
             return;
         }
     }
@@ -1735,7 +1742,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
     if (lane == 0)
         for (int k = 0; k < kDbgN; ++k) atomicAdd(&g_ewk_dbg[k], (unsigned long long)dbg[k]);
 #endif
-    score_tail<RING>(a, smem, listed);
+    if constexpr (RING != 0) score_tail<RING>(a, smem, listed);   // (linear: k_rescore_linear drains the list)
 }
 
 #ifdef EWK_TIMING
@@ -1869,6 +1876,12 @@ hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mo
         }
         hipLaunchKernelGGL((k_score_f32<0, 0>), dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, b);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_rescore_linear(const ScoreArgs& a, hipStream_t s) {
+    if (a.n_seg <= 0 || !a.rs_slots) return hipSuccess;
+    hipLaunchKernelGGL(k_rescore_linear, dim3(kScoreGridMax), dim3(64 * WAVES), LDS_BYTES, s, a);
     return hipGetLastError();
 }
 

@@ -553,13 +553,13 @@ __device__ __forceinline__ bool rs_pending(const RsArgs& a) {
 // something the last one reads (a listed segment, a finished slot, or -- with a poll mirror --
 // any score) pays it.  `listed`: lane 0 of a wave that did.
 template <int RING>
-__device__ void score_tail(const ScoreArgs& a, unsigned char* smem, bool listed) {
+__device__ void score_tail(const ScoreArgs& a, unsigned char* smem, bool listed, bool drain = true) {
     int* flag = reinterpret_cast<int*>(smem + L_WG);   // [0] last, [1 + wave] listed, [1 + WAVES] pending
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const RsArgs ra = rs_args(a);
     bool loaded = false;
     __syncthreads();   // every wave is done with the float32 tables and scratch
-    if (a.rs_slots) {
+    if (a.rs_slots && drain) {   // (drain = false: a ring workgroup without a segment, at the start of the tick)
         if (threadIdx.x == 0) flag[1 + WAVES] = rs_pending(ra);
         __syncthreads();
         if (flag[1 + WAVES]) {
@@ -619,4 +619,12 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem, bool listed)
         // fence above (after the last arrival) acquired them for this workgroup
         for (int i = threadIdx.x; i < nq; i += blockDim.x) dst[i] = src[i];
     }
+}
+
+// Linear batches: the list of a k_score_f32<0> launch is drained by this launch right after
+// it (stream-ordered: the list is complete), so the batch scorer itself makes no call and keeps
+// its register allocation; every workgroup drains, the last one out resets the counters.
+__global__ __launch_bounds__(64 * WAVES, 1) void k_rescore_linear(ScoreArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    score_tail<0>(a, smem, false, true);
 }

@@ -117,7 +117,7 @@ def test_vanishing_mean_wakeword_facade(streams, template):
         ww.waitforit()
     from easywakeword_amd._lib import EVENT_DTYPE
     ev = np.array([tuple(x) for x in seen], dtype=EVENT_DTYPE)
-    ref_n = len(run_stream(pcm, GateConfig(**GATE)).events)
-    assert len(ev) == ref_n
+    ev = ev[ev["tick"] <= len(pcm) // 1600]   # the source goes on with zeros past the stream's end
+    assert len(ev) == len(run_stream(pcm, GateConfig(**GATE)).events)
     tm, ts = ww._matcher.reference_mfcc_mean, ww._matcher.reference_mfcc_std
     assert _check(ev, pcm, (tm, ts)) >= 1
