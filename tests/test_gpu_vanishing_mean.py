@@ -56,7 +56,7 @@ def _check(events, pcm, template):
         s = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
         assert score_close(float(e["score"]), s, SCORE_TOL), (int(e["tick"]), float(e["score"]), s)
         assert bool(e["match"]) == (s >= 75.0)
-        if np.linalg.norm(cm) < 64.0:
+        if np.linalg.norm(cm) < 63.5:   # (the engine lists |float32 mean| < 64)
             small += 1
             assert e["flags"] & 2, "a vanishing-mean event must be decided by the fp64 path"
     return small
