@@ -10,7 +10,11 @@ SRCS="ewk_mfcc.hip ewk_gate.hip ewk_level3.hip ewk_engine.cpp ewk_tables.cpp"
 for f in easywakeword_amd/csrc/ewk_gather.hip; do   # sources that older revisions lack
   if [ "$REV" = "WT" ] || git -C "$R" cat-file -e "$REV:$f" 2>/dev/null; then SRCS="$SRCS $(basename $f)"; fi
 done
-for s in $SRCS ewk_internal.h ewk_gate.h; do
+HDRS="ewk_internal.h ewk_gate.h"
+for h in ewk_rescore.h; do   # headers that older revisions lack
+  if [ "$REV" = "WT" ] || git -C "$R" cat-file -e "$REV:easywakeword_amd/csrc/$h" 2>/dev/null; then HDRS="$HDRS $h"; fi
+done
+for s in $SRCS $HDRS; do
   f=easywakeword_amd/csrc/$s
   if [ "$REV" = "WT" ]; then cp "$R/$f" "$T/$f"; else git -C "$R" show "$REV:$f" > "$T/$f"; fi
 done
