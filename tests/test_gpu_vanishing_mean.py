@@ -41,7 +41,7 @@ def template():
     return mfcc_ref.extract_mfcc(synth.load_word())
 
 
-def _check(events, pcm, template):
+def _check(events, pcm, template, threshold=75.0):
     """events of one stream (tick order) vs the oracle gate + scorer; returns the number of
     |mean| < 64 events checked (each must carry EWK_EV_RESCORED)."""
     tm, ts = template
@@ -55,7 +55,7 @@ def _check(events, pcm, template):
         cm, cs = mfcc_ref.extract_mfcc(r.audio)
         s = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
         assert score_close(float(e["score"]), s, SCORE_TOL), (int(e["tick"]), float(e["score"]), s)
-        assert bool(e["match"]) == (s >= 75.0)
+        assert bool(e["match"]) == (s >= threshold)
         if np.linalg.norm(cm) < 63.5:   # (the engine lists |float32 mean| < 64)
             small += 1
             assert e["flags"] & 2, "a vanishing-mean event must be decided by the fp64 path"
@@ -120,4 +120,4 @@ def test_vanishing_mean_wakeword_facade(streams, template):
     ev = ev[ev["tick"] <= len(pcm) // 1600]   # the source goes on with zeros past the stream's end
     assert len(ev) == len(run_stream(pcm, GateConfig(**GATE)).events)
     tm, ts = ww._matcher.reference_mfcc_mean, ww._matcher.reference_mfcc_std
-    assert _check(ev, pcm, (tm, ts)) >= 1
+    assert _check(ev, pcm, (tm, ts), threshold=101.0) >= 1   # the facade's threshold: nothing matches
