@@ -760,8 +760,8 @@ static int score_pending(ewk_engine* e, hipStream_t ss, const int32_t* n_events)
     a.n_seg = e->ev_cap;
     a.work = e->d_work + 1;            // ring-mode counters (zeroed at create, re-armed by the tick end)
     a.rs_ctl = e->d_work + 8;
-    // the scorer's workgroups re-score the listed segments in fp64 and the last one out advances
-    // the watermark (no second launch per tick)
+    // k_rescore_ring (after the scorer) re-scores the listed segments in fp64 and its last
+    // workgroup out advances the watermark and writes the poll mirror
     a.adv_ev_base = e->evc_bank(e->bank) + 2;
     HIP_TRY(ensure_poll_region(e));
     a.mirror = e->d_poll + e->bank * kPollRegion;
@@ -770,6 +770,10 @@ static int score_pending(ewk_engine* e, hipStream_t ss, const int32_t* n_events)
     {
         ProfScope ps(e, 0, ss);
         HIP_TRY(launch_score_f32(e->d_tab, a, e->n_streams >= kRingWaveStreams ? 2 : 1, ss));
+    }
+    {
+        ProfScope ps(e, 1, ss);
+        HIP_TRY(launch_rescore_ring(a, ss));
     }
     return EWK_OK;
 }

@@ -135,6 +135,7 @@ struct ScoreArgs {
 hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mode, hipStream_t s);
 // fp64 re-score of what a linear launch listed (ring launches drain their list themselves)
 hipError_t launch_rescore_linear(const ScoreArgs& a, hipStream_t s);
+hipError_t launch_rescore_ring(const ScoreArgs& a, hipStream_t s);
 // streams from which a tick's events are scored one segment per wave (ring_mode 2)
 constexpr int kRingWaveStreams = 65536;
 // ScoreArgs::order holds n_seg indices followed by kLptScratch ints of bucket counters

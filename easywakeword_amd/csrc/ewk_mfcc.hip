@@ -1715,10 +1715,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
         if ((int)blockIdx.x < r_count) r_ev = a.events[r_base + blockIdx.x];
         // one segment per workgroup: a workgroup without one skips the table fill (most of
         // a quiet tick's 256 workgroups)
-        if (MODE == 1 && (int)blockIdx.x >= r_count) {
-            score_tail<RING>(a, smem, false, false);   // nothing can be listed yet: count out at once
-            return;
-        }
+        if (MODE == 1 && (int)blockIdx.x >= r_count) return;   // (k_rescore_ring ends the tick)
     }
     // ---- cooperative table load (global -> LDS), per-lane rows transposed
     {
@@ -1829,8 +1826,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
             __syncthreads();
             idx = wg_idx[0];
         }
-        score_tail<RING>(a, smem, listed);
-        return;
+        return;   // k_rescore_ring drains the re-score list and ends the tick
     }
 #ifdef EWK_TIMING
     uint64_t dbg[kDbgN] = {};
@@ -1886,7 +1882,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
     if (lane == 0)
         for (int k = 0; k < kDbgN; ++k) atomicAdd(&g_ewk_dbg[k], (unsigned long long)dbg[k]);
 #endif
-    if constexpr (RING != 0) score_tail<RING>(a, smem, listed);   // (linear: k_rescore_linear drains the list)
+    (void)listed;   // the list is drained by k_rescore_linear / k_rescore_ring, launched after this kernel
 }
 
 #ifdef EWK_TIMING
@@ -2026,6 +2022,15 @@ hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mo
 hipError_t launch_rescore_linear(const ScoreArgs& a, hipStream_t s) {
     if (a.n_seg <= 0 || !a.rs_slots) return hipSuccess;
     hipLaunchKernelGGL(k_rescore_linear, dim3(kScoreGridMax), dim3(64 * WAVES), LDS_BYTES, s, a);
+    return hipGetLastError();
+}
+
+// After every ring-mode scorer launch (also without a template: the tick end re-arms the
+// counters and advances the watermark).
+hipError_t launch_rescore_ring(const ScoreArgs& a, hipStream_t s) {
+    if (a.n_seg <= 0) return hipSuccess;
+    if (a.pcm16) hipLaunchKernelGGL(k_rescore_ring<2>, dim3(kScoreGridRing), dim3(64 * WAVES), LDS_BYTES, s, a);
+    else hipLaunchKernelGGL(k_rescore_ring<1>, dim3(kScoreGridRing), dim3(64 * WAVES), LDS_BYTES, s, a);
     return hipGetLastError();
 }
 

@@ -80,10 +80,12 @@ constexpr int RS_WAVE_BYTES = RS_XB + NMEL * kRsFrames * 4;
 static_assert(RS_WAVES + WAVES * RS_WAVE_BYTES <= L_WG, "the re-score carve must end below the workgroup flags");
 static_assert(NMFCC == 20 && kRsFrames == 8, "the DCT lane split assumes 20 coefficients and 8-frame chunks");
 
+// Between a wave's LDS writes and its other lanes' reads: LDS operations of one wave execute in
+// program order, so a compiler barrier suffices (a wavefront-scope fence would also wait for
+// the next frame's sample loads, rs_chunk).
 __device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    asm volatile("" ::: "memory");
 }
 
 // A segment's samples for the fp64 path (linear batch or wrap-aware ring slice).
@@ -94,13 +96,6 @@ struct SegView {
     int64_t ring;         // 0 = linear
     int32_t len;
 };
-
-__device__ __forceinline__ float seg_sample(const SegView& v, int q) {
-    if (q < 0 || q >= v.len) return 0.0f;   // stft(center=True, pad_mode='constant')
-    int64_t idx = v.start + q;
-    if (v.ring && idx >= v.ring) idx -= v.ring;
-    return v.p16 ? (float)v.p16[idx] * (1.0f / 32768.0f) : v.p[idx];
-}
 
 template <int RING>
 __device__ __forceinline__ SegView rs_view(const RsArgs& a, int seg) {
@@ -170,16 +165,56 @@ __device__ void rs_load_tables(const Tables64* __restrict__ tb, unsigned char* s
 
 // One frame t of the segment -> column f of the chunk's log-mel tile (split at theta_s),
 // with the running max, the ambiguity flag (|x - theta_s| <= W) and the NaN flag.
-__device__ __forceinline__ void rs_frame(const SegView& v, int t, const RsLane& c, unsigned char* wbuf,
+// A segment's samples through a buffer descriptor (as the float32 pass, SegSrc): the range
+// check returns 0 for an offset of -1, so a frame's eight loads are branch-free and all in
+// flight at once (per-sample bounds branches put a vmcnt wait behind every load).
+template <int RING>
+struct RsSrc {
+    __amdgpu_buffer_rsrc_t rsrc;   // linear: the segment; ring: the whole stream ring
+    int32_t len, start, ring;
+};
+template <int RING>
+__device__ __forceinline__ RsSrc<RING> rs_src(const SegView& v) {
+    RsSrc<RING> r;
+    const void* p = RING == 2 ? (const void*)v.p16 : (const void*)(RING ? v.p : v.p + v.start);
+    const uint64_t bu = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)bu), hi = __builtin_amdgcn_readfirstlane((uint32_t)(bu >> 32));
+    const int32_t n = __builtin_amdgcn_readfirstlane(RING ? (int32_t)v.ring : v.len);
+    r.rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                               n * (RING == 2 ? 2 : 4), 0x00020000);
+    r.len = __builtin_amdgcn_readfirstlane(v.len);
+    r.start = __builtin_amdgcn_readfirstlane((int32_t)v.start);
+    r.ring = n;
+    return r;
+}
+template <int RING>
+__device__ __forceinline__ float rs_sample(const RsSrc<RING>& v, int q) {
+    const bool in = (unsigned)q < (unsigned)v.len;   // stft(center=True, pad_mode='constant')
+    int phys = q;
+    if (RING) phys = q + v.start >= v.ring ? q + v.start - v.ring : q + v.start;
+    const int off = in ? phys * (RING == 2 ? 2 : 4) : -1;
+    if (RING == 2) return (float)(short)__builtin_amdgcn_raw_buffer_load_b16(v.rsrc, off, 0, 0) * (1.0f / 32768.0f);
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(v.rsrc, off, 0, 0));
+}
+// The eight samples lane j needs of frame t (x[2n], x[2n + 1] for n = j + 64 r), requested one
+// frame ahead of their use (rs_chunk), so a frame's loads wait behind the previous frame's FFT.
+template <int RING>
+__device__ __forceinline__ void rs_load(const RsSrc<RING>& v, int t, int lane, float (&s)[8]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int q = t * HOP - NFFT / 2 + 2 * (lane + 64 * r);
+        s[2 * r] = rs_sample(v, q);
+        s[2 * r + 1] = rs_sample(v, q + 1);
+    }
+}
+
+__device__ __forceinline__ void rs_frame(const float (&smp)[8], const RsLane& c, unsigned char* wbuf,
                                          const unsigned char* smem, int lane, int f, double theta_s, double W,
                                          double& mx, bool& amb, bool& nanf) {
     double2* buf = reinterpret_cast<double2*>(wbuf + RS_BUF);
     double2 x[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int q = t * HOP - NFFT / 2 + 2 * (lane + 64 * r);
-        x[r] = make_double2(c.win[2 * r] * (double)seg_sample(v, q), c.win[2 * r + 1] * (double)seg_sample(v, q + 1));
-    }
+    for (int r = 0; r < 4; ++r) x[r] = make_double2(c.win[2 * r] * (double)smp[2 * r], c.win[2 * r + 1] * (double)smp[2 * r + 1]);
     // radix-4 Stockham autosort: v[r] = d[j + 64 r], v[r] *= W_{4 Ns}^{r (j % Ns)}, DFT4,
     // V[r] -> d'[(j / Ns) 4 Ns + j % Ns + r Ns]; natural order after Ns = 64
 #pragma unroll
@@ -303,14 +338,22 @@ __device__ __forceinline__ double wave_max_d(double x) {
 
 // One chunk (frames 8c .. 8c + n - 1): lane k < 20 returns its 7 sums {rA, rB, sA, sB, sAA,
 // sAB, sBB} (shift = the chunk's first frame); mx / n / flags are wave-uniform.
-__device__ void rs_chunk(const SegView& v, int T, int c, double theta_s, double W, const RsLane& cl,
+template <int RING>
+__device__ void rs_chunk(const RsSrc<RING>& v, int T, int c, double theta_s, double W, const RsLane& cl,
                          const unsigned char* smem, unsigned char* wbuf, int lane, double (&pv)[7], double& mx,
                          int& n, int& flags) {
     const int t0 = c * kRsFrames;
     n = min(kRsFrames, T - t0);
     double m = -INFINITY;
     bool amb = false, nanf = false;
-    for (int f = 0; f < n; ++f) rs_frame(v, t0 + f, cl, wbuf, smem, lane, f, theta_s, W, m, amb, nanf);
+    float cur[8], nxt[8];
+    rs_load(v, t0, lane, cur);
+    for (int f = 0; f < n; ++f) {
+        if (f + 1 < n) rs_load(v, t0 + f + 1, lane, nxt);
+        rs_frame(cur, cl, wbuf, smem, lane, f, theta_s, W, m, amb, nanf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cur[i] = nxt[i];
+    }
     double A[8], B[8];
     rs_dct(smem, wbuf, lane, A, B);
     const double rA = A[0], rB = B[0];
@@ -362,7 +405,7 @@ __device__ __forceinline__ void rs_merge(RsAcc& s, const double (&pv)[7], int n)
 template <int RING>
 __device__ void rs_finish(const RsArgs& a, RsSlot* sp, int seg, int T, float theta_s32, const RsPart* parts,
                           const RsLane& cl, const unsigned char* smem, unsigned char* wbuf, int lane) {
-    const SegView v = rs_view<RING>(a, seg);
+    const RsSrc<RING> v = rs_src<RING>(rs_view<RING>(a, seg));
     const int nch = (T + kRsFrames - 1) / kRsFrames;
     const double theta_s = (double)theta_s32;
     double mx = -INFINITY;
@@ -518,7 +561,7 @@ __device__ __attribute__((noinline)) bool rs_drain(const RsArgs& a, unsigned cha
             finished = true;
             continue;
         }
-        const SegView v = rs_view<RING>(a, seg);
+        const RsSrc<RING> v = rs_src<RING>(rs_view<RING>(a, seg));
         double pv[7], mx;
         int n, flags;
         rs_chunk(v, T, unit, (double)theta_s, kRsWindow, cl, smem, wbuf, lane, pv, mx, n, flags);
@@ -627,4 +670,15 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem, bool listed,
 __global__ __launch_bounds__(64 * WAVES, 1) void k_rescore_linear(ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     score_tail<0>(a, smem, false, true);
+}
+
+// Ring mode (a streaming tick): the same, right after the tick's scorer launch.  Every listed
+// segment is known when it starts, so all its workgroups drain from the first cycle (inside the
+// scorer, workgroups that ran out of float32 work before the last listings counted out, and the
+// last one drained the rest alone: 0.07 -> 0.78 ms per 8,192-stream tick); its last workgroup
+// ends the tick (counters, event watermark, poll mirror).
+template <int RING>
+__global__ __launch_bounds__(64 * WAVES, 1) void k_rescore_ring(ScoreArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    score_tail<RING>(a, smem, false, true);
 }

@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round 4, ring re-score sessions.  Every step under its own time limit; a heartbeat line
+# every 30 s keeps a long test from reading as silent.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+TAG=${TAG:-r04b}
+( while true; do sleep 30; echo "[hb $(date +%T)] $(tail -c 200 gpurun_out/${TAG}_cur.log 2>/dev/null | tail -1)"; done ) &
+HB=$!
+trap "kill $HB" EXIT
+MODE=${1:-stream}
+if [ "$MODE" = stream ]; then   # the streaming legs only (8,192 and 131,072 streams), kernel times per tick
+  timeout -k 10 400 python bench.py --steps 3 --warmup 2 --no-cpu-baseline --fixed-len 0 --short-len 0 \
+     --confirm-batch 0 --no-host-ingest --max-streams 0 --big-ticks 100 > gpurun_out/${TAG}_cur.log 2>&1
+  rc=$?; cp gpurun_out/${TAG}_cur.log gpurun_out/${TAG}_stream.log; echo "stream bench rc=$rc"
+  python scripts/stream_line.py gpurun_out/${TAG}_stream.log 2>/dev/null || tail -c 2000 gpurun_out/${TAG}_stream.log
+  exit $rc
+fi
+if [ "$MODE" = test ]; then   # GPU tests (-k K optional)
+  K=${2:+-k $2}
+  timeout -k 10 1000 python -u -m pytest tests -v -m gpu -x -p no:cacheprovider --durations=15 --timeout 400 --timeout-method thread $K > gpurun_out/${TAG}_cur.log 2>&1
+  rc=$?; cp gpurun_out/${TAG}_cur.log gpurun_out/${TAG}_pytest_gpu.log; echo "pytest rc=$rc"; tail -25 gpurun_out/${TAG}_pytest_gpu.log
+  exit $rc
+fi
+if [ "$MODE" = rsprobe ]; then   # per-tick re-score load and time (scripts/rescore_ring_probe.py)
+  timeout -k 10 300 python -u scripts/rescore_ring_probe.py ${2:-8192} ${3:-60} > gpurun_out/${TAG}_cur.log 2>&1
+  rc=$?; cp gpurun_out/${TAG}_cur.log gpurun_out/${TAG}_rsprobe.log; echo "rsprobe rc=$rc"; tail -50 gpurun_out/${TAG}_rsprobe.log
+  exit $rc
+fi

@@ -69,3 +69,12 @@ for lo_, hi_ in ((0, 50), (50, 100), (100, 200), (200, 400), (400, 1e9)):
         print(f"streaming |mean| in [{lo_}, {hi_}): {int(sel.sum())} scored, |dscore| vs fp64 max {d[sel].max():.3e} "
               f"median {np.median(d[sel]):.3e}")
 print("NaN agreement:", bool(np.array_equal(np.isnan(sc2), np.isnan(sc64))))
+# the ring path's own scores (StreamEngine, cooperative ring scorer + k_rescore_ring) vs the fp64 path
+dr = np.abs(pick["score"] - sc64)
+okr = np.isfinite(pick["score"]) & np.isfinite(sc64)
+for lo_, hi_ in ((0, 50), (50, 64), (64, 100), (100, 200), (200, 400), (400, 1e9)):
+    sel = okr & (mn >= lo_) & (mn < hi_)
+    if sel.any():
+        print(f"ring path |mean| in [{lo_}, {hi_}): {int(sel.sum())} events, |dscore| vs fp64 max {dr[sel].max():.3e} "
+              f"median {np.median(dr[sel]):.3e}, re-scored {int(np.sum((pick['flags'][sel] & 2) != 0))}")
+print("ring NaN agreement:", bool(np.array_equal(np.isnan(pick["score"]), np.isnan(sc64))))
