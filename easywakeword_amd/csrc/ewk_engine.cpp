@@ -35,13 +35,14 @@ template <typename T>
 struct DevBuf {
     T* p = nullptr;
     size_t cap = 0;   // elements
+    unsigned flags = 0;   // hipExtMallocWithFlags flags (0: hipMalloc)
     hipError_t reserve(size_t n) {
         if (n <= cap) return hipSuccess;
         if (p) (void)hipFree(p);
         p = nullptr;
         cap = 0;
         size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
-        hipError_t e = hipMalloc(&p, bytes);
+        hipError_t e = flags ? hipExtMallocWithFlags((void**)&p, bytes, flags) : hipMalloc(&p, bytes);
         if (e == hipSuccess) cap = n;
         return e;
     }
@@ -52,6 +53,7 @@ struct DevBuf {
     }
 };
 
+constexpr int kWorkInts = 32;          // ewk_engine::d_work
 constexpr int32_t kPollChunk = 1024;   // events copied speculatively with the counters
 constexpr size_t kPollRegion = 16 + (size_t)kPollChunk * sizeof(ewk_event);   // per bank: counters + chunk
 
@@ -82,12 +84,13 @@ struct ewk_engine {
 
     // fp64 re-score (ewk_rescore.h): slots of listed segments and the chunk part pool, shared
     // by linear and ring launches (which never run concurrently: join_scoring)
-    DevBuf<RsSlot> rs_slots;        // zeroed: nclaim 0 = not published
-    DevBuf<RsPart> rs_parts;
+    DevBuf<RsSlot> rs_slots;
+    DevBuf<int32_t> rs_serial;      // serial slots of a launch
+    DevBuf<RsPart> rs_parts;        // uncached (ScoreArgs::rs_ctl)
     int32_t rs_cap = 0;             // slots
     int32_t rs_part_cap = 0;        // part records (a slot that finds the pool full runs serially)
-    // [0] linear work, [1] ring work, [4..5] event-count snapshots, [8..11] ring re-score
-    // counters (ScoreArgs::rs_ctl), [12..15] linear re-score counters
+    // [0] linear work, [1] ring work, [4..5] event-count snapshots, [16..23] ring re-score
+    // counters (ScoreArgs::rs_ctl), [24..31] linear re-score counters
     int32_t* d_work = nullptr;
     int32_t* d_compact = nullptr;   // ewk_compact_positives block counts / offsets
     int32_t compact_cap = 0;        // ... in blocks
@@ -227,6 +230,7 @@ static hipError_t reserve_rescore(ewk_engine* e, int32_t n_seg) {
     if (err != hipSuccess) return err;
     err = e->rs_slots.reserve((size_t)n_seg);
     if (err == hipSuccess) err = hipMemset(e->rs_slots.p, 0, (size_t)n_seg * sizeof(RsSlot));
+    if (err == hipSuccess) err = e->rs_serial.reserve((size_t)n_seg);
     if (err != hipSuccess) return err;
     err = e->order.reserve((size_t)n_seg + kLptScratch);
     if (err != hipSuccess) return err;
@@ -240,6 +244,7 @@ static hipError_t reserve_parts(ewk_engine* e, int32_t n) {
     hipError_t err = hipSuccess;
     if (e->stream) err = hipStreamSynchronize(e->stream);
     if (err == hipSuccess && e->sstream) err = hipStreamSynchronize(e->sstream);
+    e->rs_parts.flags = hipDeviceMallocUncached;
     if (err == hipSuccess) err = e->rs_parts.reserve((size_t)n);
     if (err == hipSuccess) e->rs_part_cap = n;
     return err;
@@ -304,6 +309,7 @@ void ewk_destroy(ewk_engine* e) {
     (void)hipFree(e->d_tab64);
     (void)hipFree(e->d_tmpl);
     e->rs_slots.release();
+    e->rs_serial.release();
     e->rs_parts.release();
     (void)hipFree(e->d_work);
     (void)hipFree(e->d_compact);
@@ -431,8 +437,8 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
     if ((err = hipMalloc(&e->d_tmpl, 2 * NMFCC * sizeof(float))) != hipSuccess) return bail(err, "template");
     if ((err = reserve_rescore(e, 4096)) != hipSuccess) return bail(err, "rescore slots");
     if ((err = reserve_parts(e, 16384)) != hipSuccess) return bail(err, "rescore parts");
-    if ((err = hipMalloc(&e->d_work, 16 * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
-    if ((err = hipMemset(e->d_work, 0, 16 * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
+    if ((err = hipMalloc(&e->d_work, kWorkInts * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
+    if ((err = hipMemset(e->d_work, 0, kWorkInts * sizeof(int32_t))) != hipSuccess) return bail(err, "work counter");
     if (n_streams > 0) {
         const size_t ring_bytes = (size_t)n_streams * e->sring_len * e->ring_es;
         if ((err = hipMalloc(&e->d_ring, ring_bytes)) != hipSuccess) return bail(err, "ring");
@@ -546,8 +552,9 @@ static ScoreArgs base_args(ewk_engine* e) {
     a.uu_s32 = e->uu_s32;
     a.threshold = e->cfg.similarity_threshold;
     a.rescore_margin = e->cfg.rescore_margin;
-    a.rs_ctl = e->d_work + 12;
+    a.rs_ctl = e->d_work + 24;
     a.rs_slots = e->has_tmpl ? e->rs_slots.p : nullptr;
+    a.rs_serial = e->rs_serial.p;
     a.rs_cap = e->rs_cap;
     a.rs_parts = e->rs_parts.p;
     a.rs_part_cap = e->rs_part_cap;
@@ -737,7 +744,7 @@ int ewk_reset_streams(ewk_engine* e) {
         x.last_silent = 1;
     }
     HIP_TRY(hipMemcpyAsync(e->d_st, st.data(), st.size() * sizeof(GateStream), hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemsetAsync(e->d_work, 0, 16 * sizeof(int32_t), s));
+    HIP_TRY(hipMemsetAsync(e->d_work, 0, kWorkInts * sizeof(int32_t), s));
     zero_event_state(e);
     HIP_TRY(hipStreamSynchronize(s));
     e->tick = 0;
@@ -759,7 +766,7 @@ static int score_pending(ewk_engine* e, hipStream_t ss, const int32_t* n_events)
     a.ev_base0 = e->ev_base0[e->bank];
     a.n_seg = e->ev_cap;
     a.work = e->d_work + 1;            // ring-mode counters (zeroed at create, re-armed by the tick end)
-    a.rs_ctl = e->d_work + 8;
+    a.rs_ctl = e->d_work + 16;
     // k_rescore_ring (after the scorer) re-scores the listed segments in fp64 and its last
     // workgroup out advances the watermark and writes the poll mirror
     a.adv_ev_base = e->evc_bank(e->bank) + 2;

@@ -61,18 +61,20 @@ void build_tables(Tables* t);
 void build_tables64(Tables64* t);
 
 // fp64 re-score (csrc/ewk_rescore.h).  A segment the float32 pass cannot decide alone is
-// listed in a slot; its 8-frame chunks are claimed by any wave that has run out of float32
-// work (every scorer workgroup drains the list before it counts itself out, and the last one
-// drains what is left), each chunk's sums land in a part record, and the wave finishing a
-// slot's last chunk combines them in chunk order.
+// listed in a slot and its 8-frame chunks get consecutive part records; a launch after the
+// scorer (k_rescore_linear / k_rescore_ring) claims the chunks with one atomic each (part
+// record g -> its slot), each chunk's sums land in its part record, and the wave finishing a
+// slot's last chunk combines them in chunk order.  A slot that finds the part pool full (or
+// every slot of ewk_score_segments_f64) is serial: one wave runs its chunks in order.
 constexpr int kRsFrames = 8;   // frames per re-score chunk
+constexpr int kRsCtl = 8;      // ints of ScoreArgs::rs_ctl
 struct RsSlot {
     int32_t seg;       // segment (linear) or event (ring) index
     int32_t T;         // frames
-    int32_t nclaim;    // claimable units: chunks, or 1 for a serial slot; published last (0 = not ready)
+    int32_t nclaim;    // chunks (1 for a serial slot)
     int32_t base;      // first part record of the slot (pooled slots)
-    int32_t cursor;    // units claimed (atomic)
-    int32_t done;      // chunks finished (atomic)
+    int32_t pad;
+    int32_t done;      // chunks finished (atomic; zeroed by the lister)
     float theta_s;     // speculative top_db clamp: the float32 pass's log-mel max - 80 dB
     int32_t serial;    // 1: one wave runs every chunk in order (no part records)
 };
@@ -81,6 +83,8 @@ struct RsPart {                 // one chunk: per coefficient k, rA rB sA sB sAA
     double mx;                  // log-mel max of the chunk's frames
     int32_t n;                  // frames
     int32_t flags;              // 1: a value within the ambiguity window of theta_s, 2: NaN
+    int32_t slot;               // the slot this record belongs to (-1: a failed reservation)
+    int32_t pad[3];
 };
 static_assert(sizeof(RsPart) % 16 == 0, "part records are 16-B aligned");
 
@@ -110,11 +114,15 @@ struct ScoreArgs {
     double threshold;
     double rescore_margin;
     int32_t* order;           // linear mode: work order scratch [n_seg] (longest first), nullptr = index order
-    // fp64 re-score (nullptr rs_slots: none).  rs_ctl: [0] slots listed, [1] part records
-    // reserved, [2] scan hint, [3] workgroups out; the last workgroup out zeroes them (and
-    // *work) and, in ring mode, sets *adv_ev_base = *n_events
+    // fp64 re-score (nullptr rs_slots: none).  rs_ctl (kRsCtl ints): [0] slots listed,
+    // [1] part records reserved, [2] serial slots listed, [3] workgroups out, [4] chunk claim
+    // cursor, [5] serial claim cursor; the last workgroup out of the re-score launch zeroes
+    // them (and *work) and, in ring mode, sets *adv_ev_base = *n_events.  The part records
+    // live in uncached memory (hipDeviceMallocUncached): written by one wave and read by
+    // another, on any XCD, with no L2 write-back or invalidate in between.
     int32_t* rs_ctl;
     RsSlot* rs_slots;
+    int32_t* rs_serial;       // [rs_cap] serial slots, in listing order
     int32_t rs_cap;
     int32_t rs_part_cap;
     RsPart* rs_parts;

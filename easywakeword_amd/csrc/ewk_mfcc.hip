@@ -1885,6 +1885,17 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
     (void)listed;   // the list is drained by k_rescore_linear / k_rescore_ring, launched after this kernel
 }
 
+#ifdef EWK_RS_TIMING
+}  // namespace ewk
+extern "C" int ewk_debug_rs(unsigned long long* out) {   // read and reset (debug builds only)
+    unsigned long long z[16] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ewk::g_rs_dbg), sizeof(z)) != hipSuccess) return -3;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(ewk::g_rs_dbg), z, sizeof(z)) != hipSuccess) return -3;
+    return 0;
+}
+namespace ewk {
+#endif
+
 #ifdef EWK_TIMING
 }  // namespace ewk
 extern "C" int ewk_debug_timing(unsigned long long* out) {   // read and reset (debug builds only)
@@ -1961,7 +1972,7 @@ __global__ __launch_bounds__(kLptBlock) void k_lpt_scatter(const int32_t* __rest
     __shared__ int h[kLptBuckets], base[kLptBuckets];
     if (blockIdx.x == 0 && threadIdx.x == 0) {   // the scorer's counters (no fill launches)
         *work = 0;
-        for (int i = 0; i < 4; ++i) rs_ctl[i] = 0;
+        for (int i = 0; i < kRsCtl; ++i) rs_ctl[i] = 0;
     }
     if (threadIdx.x < kLptBuckets) h[threadIdx.x] = 0;
     __syncthreads();
@@ -2011,7 +2022,7 @@ hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mo
         } else {
             b.order = nullptr;
             hipError_t e = hipMemsetAsync(a.work, 0, sizeof(int32_t), s);
-            if (e == hipSuccess) e = hipMemsetAsync(a.rs_ctl, 0, 4 * sizeof(int32_t), s);
+            if (e == hipSuccess) e = hipMemsetAsync(a.rs_ctl, 0, kRsCtl * sizeof(int32_t), s);
             if (e != hipSuccess) return e;
         }
         hipLaunchKernelGGL((k_score_f32<0, 0>), dim3(grid), dim3(64 * WAVES), LDS_BYTES, s, d_tab, b);

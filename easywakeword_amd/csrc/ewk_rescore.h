@@ -28,6 +28,15 @@
 //
 // scripts/f64_chunk_model.py is the numpy model of these index maps and algebra.
 
+// Drain counters of a -DEWK_RS_TIMING debug build (scripts/rescore_ring_probe.py reads them
+// with ewk_debug_rs); the product build compiles none of it.
+#ifdef EWK_RS_TIMING
+__device__ unsigned long long g_rs_dbg[16];
+#define EWK_RS_ADD(k, v) (void)atomicAdd(&g_rs_dbg[k], (unsigned long long)(v))
+#else
+#define EWK_RS_ADD(k, v) ((void)0)
+#endif
+
 constexpr double kRsWindow = 1e-3;   // dB; the float32 max is within ~1e-5 dB of the fp64 one
 constexpr double kRsTopDb = 80.0;
 
@@ -48,8 +57,10 @@ struct RsArgs {
     int32_t cand_f32;
     int32_t* rs_ctl;
     RsSlot* rs_slots;
+    int32_t* rs_serial;
     RsPart* rs_parts;
     int32_t rs_cap;
+    int32_t rs_part_cap;
     double* out_score;
     uint8_t* out_match;
     double* out_mean64;
@@ -62,6 +73,7 @@ __device__ __forceinline__ RsArgs rs_args(const ScoreArgs& a) {
     r.pcm = a.pcm; r.pcm16 = a.pcm16; r.offsets = a.offsets; r.lengths = a.lengths; r.events = a.events;
     r.ring_len = a.ring_len; r.tmpl = a.tmpl; r.threshold = a.threshold; r.has_template = a.has_template;
     r.cand_f32 = a.cand_f32; r.rs_ctl = a.rs_ctl; r.rs_slots = a.rs_slots; r.rs_parts = a.rs_parts;
+    r.rs_serial = a.rs_serial; r.rs_part_cap = a.rs_part_cap;
     r.rs_cap = a.rs_cap; r.out_score = a.out_score; r.out_match = a.out_match; r.out_mean64 = a.out_mean64;
     r.out_std64 = a.out_std64; r.tab64 = a.tab64;
     return r;
@@ -430,6 +442,7 @@ __device__ void rs_finish(const RsArgs& a, RsSlot* sp, int seg, int T, float the
     const double theta = mx - kRsTopDb;
     const bool nan_in = (fl & 2) != 0;
     const bool redo_all = !(fabs(theta - theta_s) <= kRsWindow);
+    if (lane == 0 && parts) { EWK_RS_ADD(6, redo_all); EWK_RS_ADD(7, nch); }
     if (!nan_in && (parts || redo_all || (fl & 1))) {
         if (!parts) acc = RsAcc();
         for (int c = 0; c < nch; ++c) {
@@ -437,6 +450,7 @@ __device__ void rs_finish(const RsArgs& a, RsSlot* sp, int seg, int T, float the
             if (!parts || redo_all || (parts[c].flags & 1)) {   // classification at the exact theta
                 double m;
                 int f;
+                if (lane == 0 && parts) EWK_RS_ADD(8, 1);
                 rs_chunk(v, T, c, theta, -1.0, cl, smem, wbuf, lane, pv, m, n, f);
             } else {
                 n = parts[c].n;
@@ -485,12 +499,12 @@ __device__ void rs_finish(const RsArgs& a, RsSlot* sp, int seg, int T, float the
                 if (a.out_match) a.out_match[seg] = (uint8_t)match;
             }
         }
-        __hip_atomic_store(&sp->nclaim, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // finished
     }
     wave_sync();
 }
 
-// List segment `seg` (lane 0 of its scoring wave, after its float32 score is written).
+// List segment `seg` (lane 0 of its scoring wave, after its float32 score is written).  Plain
+// stores: the list is read by the re-score launch that follows the scorer (stream order).
 __device__ __forceinline__ void rs_list(const ScoreArgs& a, int seg, int len, float theta_s) {
     const int s = atomicAdd(&a.rs_ctl[0], 1);
     if (s >= a.rs_cap) return;   // list full: the float32 score stands
@@ -505,50 +519,72 @@ __device__ __forceinline__ void rs_list(const ScoreArgs& a, int seg, int len, fl
     p->seg = seg;
     p->T = T;
     p->base = base;
-    p->cursor = 0;
+    p->nclaim = serial ? 1 : nch;
     p->done = 0;
     p->theta_s = theta_s;
     p->serial = serial;
-    __hip_atomic_store(&p->nclaim, serial ? 1 : nch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (serial) {
+        a.rs_serial[atomicAdd(&a.rs_ctl[2], 1)] = s;
+        for (int c = base; c < min(base + nch, a.rs_part_cap); ++c) a.rs_parts[c].slot = -1;   // (a failed reservation)
+    } else {
+        for (int c = 0; c < nch; ++c) a.rs_parts[base + c].slot = s;
+    }
 }
 
-// Lane 0: claim the next unit (a chunk, or a whole serial slot).  nclaim: 0 not yet published,
-// -1 finished, > 0 claimable units.  The scan hint moves past a prefix of slots whose units are
-// all taken.
+// Lane 0: claim the next unit -- a chunk (part record g of the reserved range, one atomic),
+// then, once every chunk is taken, a whole serial slot.
 struct RsClaim {
     int slot = -1, unit = 0, seg = 0, T = 0, base = 0, serial = 0, nclaim = 0;
     float theta_s = 0.0f;
 };
-__device__ __forceinline__ RsClaim rs_claim(const RsArgs& a) {
+__device__ __forceinline__ RsClaim rs_claim(const RsArgs& a, int n_parts, int n_serial) {
     RsClaim r;
-    const int n = min(__hip_atomic_load(&a.rs_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.rs_cap);
-    bool prefix = true;
-    for (int s = __hip_atomic_load(&a.rs_ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); s < n; ++s) {
-        RsSlot* p = a.rs_slots + s;
-        const int nc = __hip_atomic_load(&p->nclaim, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-        if (nc == 0) { prefix = false; continue; }
-        if (nc > 0) {
-            const int u = __hip_atomic_fetch_add(&p->cursor, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (u < nc) {
-                r.slot = s; r.unit = u; r.nclaim = nc;
-                r.seg = p->seg; r.T = p->T; r.base = p->base; r.serial = p->serial; r.theta_s = p->theta_s;
-                return r;
-            }
+    int s = -1;
+    for (;;) {
+        const int g = __hip_atomic_fetch_add(&a.rs_ctl[4], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        EWK_RS_ADD(12, 1);
+        if (g >= n_parts) break;
+        s = a.rs_parts[g].slot;
+        if (s >= 0) {
+            const RsSlot* p = a.rs_slots + s;
+            r.unit = g - p->base;
+            break;
         }
-        if (prefix) __hip_atomic_fetch_max(&a.rs_ctl[2], s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (s < 0) {   // every chunk is taken: the serial slots
+        const int q = __hip_atomic_fetch_add(&a.rs_ctl[5], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (q >= n_serial) return r;
+        s = a.rs_serial[q];
+        r.unit = 0;
+    }
+    const RsSlot* p = a.rs_slots + s;
+    r.slot = s; r.nclaim = p->nclaim;
+    r.seg = p->seg; r.T = p->T; r.base = p->base; r.serial = p->serial; r.theta_s = p->theta_s;
     return r;
+}
+
+// The list sizes of this launch (fixed while it runs: the lister was the previous launch).
+__device__ __forceinline__ int rs_n_parts(const RsArgs& a) {
+    return min(__hip_atomic_load(&a.rs_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.rs_part_cap);
+}
+__device__ __forceinline__ int rs_n_serial(const RsArgs& a) {
+    return min(__hip_atomic_load(&a.rs_ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.rs_cap);
 }
 
 // One wave drains the list until nothing is claimable; true if it finished a slot.
 template <int RING>
 __device__ __attribute__((noinline)) bool rs_drain(const RsArgs& a, unsigned char* smem, int wave, int lane) {
     unsigned char* wbuf = smem + RS_WAVES + wave * RS_WAVE_BYTES;
+    if (lane == 0) EWK_RS_ADD(0, 1);   // waves that drain
+#ifdef EWK_RS_TIMING
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+#endif
     RsLane cl;
     bool have_lane = false, finished = false;
+    const int n_parts = rs_n_parts(a), n_serial = rs_n_serial(a);
     for (;;) {
         RsClaim c;
-        if (lane == 0) c = rs_claim(a);
+        if (lane == 0) c = rs_claim(a, n_parts, n_serial);
         const int slot = __shfl(c.slot, 0, 64);
         if (slot < 0) break;
         const int unit = __shfl(c.unit, 0, 64), seg = __shfl(c.seg, 0, 64), T = __shfl(c.T, 0, 64);
@@ -557,10 +593,14 @@ __device__ __attribute__((noinline)) bool rs_drain(const RsArgs& a, unsigned cha
         if (!have_lane) { rs_lane_init(a.tab64, lane, cl); have_lane = true; }
         RsSlot* sp = a.rs_slots + slot;
         if (serial) {
+            if (lane == 0) EWK_RS_ADD(5, 1);
             rs_finish<RING>(a, sp, seg, T, theta_s, nullptr, cl, smem, wbuf, lane);
             finished = true;
             continue;
         }
+#ifdef EWK_RS_TIMING
+        const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
+#endif
         const RsSrc<RING> v = rs_src<RING>(rs_view<RING>(a, seg));
         double pv[7], mx;
         int n, flags;
@@ -571,22 +611,38 @@ __device__ __attribute__((noinline)) bool rs_drain(const RsArgs& a, unsigned cha
             for (int q = 0; q < 7; ++q) pp->v[q * NMFCC + lane] = pv[q];
         }
         if (lane == 0) { pp->mx = mx; pp->n = n; pp->flags = flags; }
-        __threadfence();   // the part record before the count (release)
+#ifdef EWK_RS_TIMING
+        if (lane == 0) { EWK_RS_ADD(1, 1); EWK_RS_ADD(2, __builtin_amdgcn_s_memrealtime() - c0); }
+#endif
+        // the part record (uncached memory) is in place before the count: no L2 write-back
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int last = 0;
         if (lane == 0) last = __hip_atomic_fetch_add(&sp->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nclaim - 1;
-        if (__shfl(last, 0, 64)) {
-            __threadfence();   // every part record of the slot (acquire)
+        if (__shfl(last, 0, 64)) {   // (the part loads below issue after the count returned)
+#ifdef EWK_RS_TIMING
+            const unsigned long long f0 = __builtin_amdgcn_s_memrealtime();
+#endif
             rs_finish<RING>(a, sp, seg, T, theta_s, a.rs_parts + base, cl, smem, wbuf, lane);
+#ifdef EWK_RS_TIMING
+            if (lane == 0) { EWK_RS_ADD(3, 1); EWK_RS_ADD(4, __builtin_amdgcn_s_memrealtime() - f0); }
+#endif
             finished = true;
         }
     }
+#ifdef EWK_RS_TIMING
+    if (lane == 0) {
+        const unsigned long long d = __builtin_amdgcn_s_memrealtime() - r0;
+        (void)atomicMax(&g_rs_dbg[10], d);
+        EWK_RS_ADD(11, d);
+    }
+#endif
     return finished;
 }
 
 // Anything listed that no wave has taken yet (thread 0)?
 __device__ __forceinline__ bool rs_pending(const RsArgs& a) {
-    const int n = min(__hip_atomic_load(&a.rs_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.rs_cap);
-    return n > __hip_atomic_load(&a.rs_ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __hip_atomic_load(&a.rs_ctl[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < rs_n_parts(a) ||
+           __hip_atomic_load(&a.rs_ctl[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < rs_n_serial(a);
 }
 
 // End of every k_score_f32 workgroup (all modes), after its float32 work: drain the re-score
@@ -606,6 +662,7 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem, bool listed,
         if (threadIdx.x == 0) flag[1 + WAVES] = rs_pending(ra);
         __syncthreads();
         if (flag[1 + WAVES]) {
+            if (threadIdx.x == 0) EWK_RS_ADD(9, 1);   // workgroups that drain
             rs_load_tables(a.tab64, smem);
             __syncthreads();
             loaded = true;
@@ -623,6 +680,9 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem, bool listed,
     }
     __syncthreads();
     if (!flag[0]) return;
+#ifdef EWK_RS_TIMING
+    const unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
+#endif
     __threadfence();   // acquire what every other workgroup released before its count
     if (a.rs_slots) {   // the last workgroup: every other has drained and counted out
         if (threadIdx.x == 0) flag[1 + WAVES] = rs_pending(ra);
@@ -635,17 +695,12 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem, bool listed,
             rs_drain<RING>(ra, smem, wave, lane);
         }
         __syncthreads();
-        // finished slots (-1) back to "not published" for the next launch
-        const int n = min(__hip_atomic_load(&a.rs_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), a.rs_cap);
-        for (int i = threadIdx.x; i < n; i += blockDim.x) a.rs_slots[i].nclaim = 0;
     }
     if (threadIdx.x == 0) {
         if (RING) *a.adv_ev_base = *a.n_events;
         *a.work = 0;
-        a.rs_ctl[0] = 0;
-        a.rs_ctl[1] = 0;
-        a.rs_ctl[2] = 0;
-        a.rs_ctl[3] = 0;
+#pragma unroll
+        for (int i = 0; i < kRsCtl; ++i) a.rs_ctl[i] = 0;
         __threadfence();
     }
     if (RING && a.mirror) {   // poll mirror: the bank's counters and first events -> pinned host memory
@@ -662,6 +717,9 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem, bool listed,
         // fence above (after the last arrival) acquired them for this workgroup
         for (int i = threadIdx.x; i < nq; i += blockDim.x) dst[i] = src[i];
     }
+#ifdef EWK_RS_TIMING
+    if (threadIdx.x == 0) EWK_RS_ADD(13, __builtin_amdgcn_s_memrealtime() - t_last);
+#endif
 }
 
 // Linear batches: the list of a k_score_f32<0> launch is drained by this launch right after

@@ -16,8 +16,8 @@ if [ "$MODE" = stream ]; then   # the streaming legs only (8,192 and 131,072 str
   exit $rc
 fi
 if [ "$MODE" = test ]; then   # GPU tests (-k K optional)
-  K=${2:+-k $2}
-  timeout -k 10 1000 python -u -m pytest tests -v -m gpu -x -p no:cacheprovider --durations=15 --timeout 400 --timeout-method thread $K > gpurun_out/${TAG}_cur.log 2>&1
+  K=${2:-}
+  timeout -k 10 1000 python -u -m pytest tests -v -m gpu -x -p no:cacheprovider --durations=15 --timeout 400 --timeout-method thread ${K:+-k "$K"} > gpurun_out/${TAG}_cur.log 2>&1
   rc=$?; cp gpurun_out/${TAG}_cur.log gpurun_out/${TAG}_pytest_gpu.log; echo "pytest rc=$rc"; tail -25 gpurun_out/${TAG}_pytest_gpu.log
   exit $rc
 fi

@@ -25,6 +25,12 @@ while t < 100:   # prefill
     se.poll()
     t += n
 se.sync()
+import ctypes
+dlib = ctypes.CDLL(os.environ.get("EWK_LIB") or os.path.join(ROOT, "easywakeword_amd", "libewk.so"))
+dbg = hasattr(dlib, "ewk_debug_rs")
+dbuf = (ctypes.c_ulonglong * 16)()
+if dbg:
+    dlib.ewk_debug_rs(dbuf)
 rows = []
 for i in range(ticks):
     k = t % period
@@ -37,6 +43,14 @@ for i in range(ticks):
     se.profile(False)
     real = ev[(ev["flags"] & 1) == 0]
     rs = real[(real["flags"] & 2) != 0]
+    if dbg:
+        dlib.ewk_debug_rs(dbuf)
+        if len(rs):
+            d = list(dbuf)
+            print(f"  tick {i}: drain waves {d[0]} wgs {d[9]} chunks {d[1]} ({d[2] / max(1, d[1]):,.0f} cyc each) "
+                  f"finishes {d[3]} ({d[4] / max(1, d[3]):,.0f} cyc each) serial {d[5]} redo_all {d[6]} "
+                  f"chunks-in-finished {d[7]} recomputed {d[8]}; drain per wave max {d[10] / 100:.0f} us mean {d[11] / 100 / max(1, d[0]):.0f} us; "
+                  f"claim scans {d[12]}; last-WG tail {d[13] / 100:.1f} us")
     T = 1 + rs["length"].astype(np.int64) // 160
     rows.append((len(real), len(rs), int(T.sum()), int(((T + 7) // 8).sum()), int(T.max()) if len(T) else 0, sc_ms * 1e3, r_ms * 1e3))
     t += 1
