@@ -26,3 +26,21 @@ if [ "$MODE" = rsprobe ]; then   # per-tick re-score load and time (scripts/resc
   rc=$?; cp gpurun_out/${TAG}_cur.log gpurun_out/${TAG}_rsprobe.log; echo "rsprobe rc=$rc"; tail -50 gpurun_out/${TAG}_rsprobe.log
   exit $rc
 fi
+if [ "$MODE" = std ]; then   # |mean| / |std| distributions and the fp32-vs-fp64 score error by |mean|, ring path too
+  timeout -k 10 600 python -u scripts/std_norm_dist.py > gpurun_out/${TAG}_cur.log 2>&1
+  rc=$?; cp gpurun_out/${TAG}_cur.log gpurun_out/${TAG}_std_norm_dist.txt; echo "std rc=$rc"; tail -25 gpurun_out/${TAG}_std_norm_dist.txt
+  exit $rc
+fi
+if [ "$MODE" = bench ]; then   # the default bench line, then its rocprofv3 kernel trace
+  timeout -k 10 900 python bench.py --steps 20 --warmup 10 > gpurun_out/${TAG}_cur.log 2>&1
+  rc=$?; cp gpurun_out/${TAG}_cur.log gpurun_out/${TAG}_bench.log; echo "bench rc=$rc"; tail -c 600 gpurun_out/${TAG}_bench.log; echo
+  [ $rc -eq 0 ] || exit $rc
+  python scripts/stream_line.py gpurun_out/${TAG}_bench.log
+  R="$PWD"; cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${TAG}_prof" -o run -- python3 "$R/bench.py" --steps 20 --warmup 10 --no-cpu-baseline --fixed-len 0 --short-len 0 > "$R/gpurun_out/${TAG}_cur.log" 2>&1
+  rc=$?; echo "rocprof rc=$rc"
+  python "$R/scripts/prof_summary.py" "$R/gpurun_out/${TAG}_prof" 10 > "$R/gpurun_out/${TAG}_kernel_stats.txt" 2>&1
+  rm -f "$R/gpurun_out/${TAG}_prof/run_kernel_trace.csv"
+  head -12 "$R/gpurun_out/${TAG}_kernel_stats.txt"; tail -3 "$R/gpurun_out/${TAG}_kernel_stats.txt"
+  exit $rc
+fi
