@@ -1078,102 +1078,6 @@ __device__ __forceinline__ float scout_tiles(const SegSrc<RING>& v, int ntile, i
     return e;
 }
 
-// Cross-segment prefetch (linear batches): while a wave finishes a segment
-// (fix-ups done, finish_stats, score epilogue -- latency-bound phases), the scout rows of the
-// next segment's first kScoutBatch tiles arrive in the wave's (free) tile region by LDS-DMA
-// (buffer_load_dword ... lds: no VGPRs), are ranked after finish_stats, and the next segment's
-// first pass is requested into registers before the epilogue -- the two memory round trips a
-// segment used to start with (scout, first stage) overlap the previous segment's tail.
-#ifndef EWK_PREFETCH
-#define EWK_PREFETCH 0
-#endif
-#ifndef EWK_DMA_STAGE
-#define EWK_DMA_STAGE 1
-#endif
-constexpr bool kPrefetch = EWK_PREFETCH;
-// EWK_DMA_STAGE: the next segment's first pass goes to the stage area by LDS-DMA too (the buffer
-// range check writes 0 for the stft padding: scripts/probes/buffer_lds_probe.hip); 0: into
-// registers (pf), stored at the next segment's start.
-constexpr bool kDmaStage = EWK_DMA_STAGE;
-struct NextPrep {
-    int ready = 0;              // the next segment's order is in spec[] and its first pass staged / in pf
-    float pf[kStageLoads];   // (unused with kDmaStage)
-};
-
-// The stage rows of the pass starting at sample q0 -> the wave's stage area by LDS-DMA (the
-// rows and skew of stage_store; a lane outside [0, len) reads 0, like stage_load).
-template <int RING>
-__device__ __forceinline__ void stage_dma(const SegSrc<RING>& v, int q0, int lane, float* stage) {
-    // linear: one address VGPR (the segment's sample q0 + lane) and the row in the SGPR offset,
-    // so no per-row address stays live (hoisted per-row addresses spilled)
-    const int base = (q0 + lane) * 4;
-#pragma unroll
-    for (int c = 0; c < kStageLoads; ++c) {
-        int off, soff = 0;
-        if (RING) {
-            const int q = q0 + 64 * c + lane;
-            const int phys = q >= v.wrap_at ? q - v.wrap_at : q + v.start;
-            off = (unsigned)q < (unsigned)v.len ? phys * 4 : -1;
-        } else {
-            off = base;
-            soff = 256 * c;
-        }
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(v.rsrc, (__attribute__((address_space(3))) void*)(stage + stg_off(c) / 4),
-                                                 4, off, soff, 0, 0);
-    }
-}
-
-template <int RING>
-__device__ __forceinline__ void scout_dma(const SegSrc<RING>& v, int ntile, int lane, float* rows) {
-#pragma unroll
-    for (int u = 0; u < kScoutBatch; ++u) {   // tile u, row q -> rows[(4 u + q) * 64 + lane]
-        if (u < ntile) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int qs = u * 16 * HOP + 640 * q + 64 + lane;
-                int off, soff = 0;
-                if (RING) {
-                    const int phys = qs >= v.wrap_at ? qs - v.wrap_at : qs + v.start;
-                    off = (unsigned)qs < (unsigned)v.len ? phys * 4 : -1;
-                } else {
-                    off = (64 + lane) * 4;
-                    soff = (u * 16 * HOP + 640 * q) * 4;
-                }
-                __builtin_amdgcn_raw_ptr_buffer_load_lds(v.rsrc, (__attribute__((address_space(3))) void*)(rows + (4 * u + q) * 64),
-                                                         4, off, soff, 0, 0);
-            }
-        }
-    }
-}
-
-// Energies of the DMA'd scout rows (ntile <= kScoutBatch tiles): lane t gets tile t's.
-__device__ __forceinline__ void scout_lds(const float* rows, int ntile, int lane, float& e) {
-#pragma unroll
-    for (int u = 0; u < kScoutBatch; ++u) {
-        if (u < ntile) {
-            float a = 0.0f;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const float x = rows[(4 * u + q) * 64 + lane];
-                a = q ? fmaf(x, x, a) : x * x;
-            }
-            const float tot = wave_sum_f(a);
-            if (lane == u) e = tot;
-        }
-    }
-}
-
-// Rank the scout estimates (lane t: tile t) into order[] (loudest first, ties by index).
-__device__ __forceinline__ void scout_rank(float e, int ntile, int lane, int* order) {
-    e = e == e ? e : 0.0f;   // NaN samples: a total order (unique ranks) all the same
-    int rank = 0;
-    for (int u = 0; u < ntile; ++u) {
-        const float eu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), u));
-        rank += (eu > e) || (eu == e && u < lane);
-    }
-    if (lane < ntile) order[rank] = lane;
-}
-
 // The next work item of a persistent wave (linear batches, ring mode 2), claimed ahead:
 // its index is requested when the current segment's last tile starts, its work-order entry
 // when that tile's passes end and its descriptor before the fix-ups, so neither the atomic
@@ -1221,18 +1125,6 @@ __device__ __forceinline__ void work_describe(const WorkCtx& c, WorkAhead& w) {
     }
 }
 
-// The segment source of a described next work item.
-template <int RING>
-__device__ __forceinline__ SegSrc<RING> next_src(const WorkCtx& c, const WorkAhead& w) {
-    const ScoreArgs& a = *c.a;
-    if (RING) {
-        const void* ring_base = RING == 2 ? (const void*)a.pcm16 : (const void*)a.pcm;
-        return make_src<RING>(static_cast<const unsigned char*>(ring_base) + (int64_t)w.stream * a.ring_len * sample_bytes(RING),
-                              w.start, a.ring_len, w.len);
-    }
-    return make_src<RING>(a.pcm, w.start, 0, w.len);
-}
-
 // Whole segment for one wave.  spec: this wave's per-tile record in LDS -- the stored
 // log-mel minimum of pass p of tile i in spec[kPassesPerTile * i + p], the tile's
 // speculative clamp in spec[kSpecRun + i] (tiles past kSpecTiles are stored unclamped and
@@ -1246,8 +1138,7 @@ __device__ __forceinline__ SegSrc<RING> next_src(const WorkCtx& c, const WorkAhe
 template <int RING>
 __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, float* scr, float* tile,
                               float* spec, int lane, const int (&lo)[8], double (&s1)[8], double (&s2)[8],
-                              float& theta_out, const WorkCtx& wc, WorkAhead& nx,
-                              NextPrep& prep EWK_DBG_PARAM) {
+                              float& theta_out, const WorkCtx& wc, WorkAhead& nx EWK_DBG_PARAM) {
     EWK_TS(tq0);
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     const int T = 1 + v.len / HOP;
@@ -1256,11 +1147,15 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     const int col = lane & 15;
     int* order = reinterpret_cast<int*>(spec + kSpecOrder);
     const bool ordered = ntile > 1 && ntile <= kSpecTiles;
-    const bool pre = prep.ready;   // scout ranked and first pass requested during the previous segment
-    prep.ready = 0;
-    if (ordered && !pre) {   // loudest-first order: lane t ranks tile t (ties by index)
-        const float e = scout_tiles(v, ntile, lane);
-        scout_rank(e, ntile, lane, order);
+    if (ordered) {   // loudest-first order: lane t ranks tile t (ties by index)
+        float e = scout_tiles(v, ntile, lane);
+        e = e == e ? e : 0.0f;   // NaN samples: a total order (unique ranks) all the same
+        int rank = 0;
+        for (int u = 0; u < ntile; ++u) {
+            const float eu = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(e), u));
+            rank += (eu > e) || (eu == e && u < lane);
+        }
+        if (lane < ntile) order[rank] = lane;
         lds_order();
     }
     EWK_TS(tq1);
@@ -1270,11 +1165,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
     float vmax = -INFINITY, vmin = INFINITY, nanp = 0.0f;
     int tile_i = ordered ? order[0] : 0;
-    if (pre) {   // the first pass's samples were requested before the previous segment's epilogue
-        if constexpr (kDmaStage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else stage_store(scr, lane, prep.pf);
-        lds_order();
-    } else {     // stage the first pass synchronously
+    {   // stage the first pass synchronously
         float r[kStageLoads];
         stage_load(v, tile_i * 16 * HOP - NFFT / 2, lane, r);
         stage_store(scr, lane, r);
@@ -1369,40 +1260,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     }
     EWK_TS(tq4);
     EWK_TADD(5, tq3, tq4);
-    // the next segment's scout rows -> this wave's tile region (free now), in flight over finish_stats
-    bool nxt = false;
-    SegSrc<RING> vn;
-    // (linear batches only: in ring mode 2 the wrap-aware addresses of the DMA rows spilled VGPRs)
-    if (kPrefetch && RING == 0 && wc.ahead && nx.state == 3 && nx.idx < wc.count) {
-        vn = next_src<RING>(wc, nx);
-        nxt = true;
-        const int ntn = ((1 + vn.len / HOP) + 15) >> 4;
-        if (ntn > 1 && ntn <= kSpecTiles) scout_dma(vn, min(ntn, kScoutBatch), lane, tile);
-    }
-    // (pd in the spec area when the next pass is DMA'd into the stage: the per-pass minima are dead)
-    finish_stats(T, cref, s1, s2, lane, reinterpret_cast<double*>(nxt && kDmaStage ? spec : scr));
-    if (nxt) {   // rank the next segment's tiles and request its first pass (lands during the epilogue)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int ntn = ((1 + vn.len / HOP) + 15) >> 4;
-        const bool orderedn = ntn > 1 && ntn <= kSpecTiles;
-        if (orderedn) {
-            float e = -1.0f;
-            scout_lds(tile, min(ntn, kScoutBatch), lane, e);
-            for (int t0 = kScoutBatch; t0 < ntn; t0 += kScoutBatch) {
-                const int left = ntn - t0;
-                if (left <= 2) scout_batch<RING, 2>(vn, t0, lane, e);
-                else if (left <= 4) scout_batch<RING, 4>(vn, t0, lane, e);
-                else scout_batch<RING, kScoutBatch>(vn, t0, lane, e);
-            }
-            lds_order();
-            scout_rank(e, ntn, lane, order);
-            lds_order();
-        }
-        const int first = orderedn ? order[0] : 0;
-        if constexpr (kDmaStage) stage_dma(vn, first * 16 * HOP - NFFT / 2, lane, scr);
-        else stage_load(vn, first * 16 * HOP - NFFT / 2, lane, prep.pf);
-        prep.ready = 1;
-    }
+    finish_stats(T, cref, s1, s2, lane, reinterpret_cast<double*>(scr));
     EWK_TS(tq5);
     EWK_TADD(6, tq4, tq5);
 }
@@ -1833,14 +1691,12 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
 #endif
     const WorkCtx wc = {&a, base, count, true};
     WorkAhead nx;
-    NextPrep prep;
     for (;;) {
         EWK_TS(tw0);
         if (nx.state != 3) {   // nothing claimed ahead (first segment, or after a skipped event)
             work_claim<RING>(wc, nx, lane);
             work_order<RING>(wc, nx);
             work_describe<RING>(wc, nx);
-            prep.ready = 0;
         }
         nx.state = 0;
         if (nx.idx >= count) break;
@@ -1860,7 +1716,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
 
         double st1[8], st2[8];
         float theta_s;
-        segment_stats(v, smem, scr, tile, spec, lane, lo, st1, st2, theta_s, wc, nx, prep EWK_DBG_ARG);
+        segment_stats(v, smem, scr, tile, spec, lane, lo, st1, st2, theta_s, wc, nx EWK_DBG_ARG);
         EWK_TS(tw2);
 
         // ---- lane k < 20 holds coefficient k's mean / std (fp32-rounded like the reference's)
