@@ -1,16 +1,20 @@
 // ewk_rescore.h -- the fp64 re-score of the segments the float32 pass cannot decide alone
 // (near the threshold, very short, nearly stationary, or with a vanishing MFCC mean vector:
-// see score_epilogue), run by k_score_f32's own workgroups after their float32 work.
-// Included by ewk_mfcc.hip after the score arithmetic; device code only.
+// see score_epilogue), run by a launch right after the scorer (k_rescore_linear,
+// k_rescore_ring).  Included by ewk_mfcc.hip after the score arithmetic; device code only.
 //
 // This is the float64 candidate path of the reference (wakeword.py:509-513 hands float64 ring
 // slices to WordMatcher.extract_mfcc, wakeword.py:544-567 -> librosa 0.11.0 feature.mfcc with
 // complex128 stft, float32 Slaney weights, float64 power_to_db and DCT, numpy mean / std).
 //
-// Work split.  A listed segment is a slot; its frames are cut into 8-frame chunks that any
-// wave out of float32 work claims (every workgroup drains the list before it counts itself
-// out; the last one out drains what is left, so no workgroup ever waits on another).  One
-// chunk = one wave, one frame at a time over its 64 lanes:
+// Work split.  A listed segment is a slot; its frames are cut into 8-frame chunks whose part
+// records are consecutive in a pool (the lister reserves them with one atomic and writes each
+// record's slot index).  Every wave of the re-score launch claims part record g with one atomic
+// on a shared cursor, runs that chunk and counts it done on its slot; the wave finishing a
+// slot's last chunk merges the slot.  The part records live in uncached memory, so a record
+// written by one wave is read by another on any XCD without an L2 write-back or invalidate
+// (round 4: an agent-scope acquire per scanned slot invalidated the XCD's L2 on every claim,
+// and a burst tick took 5 ms).  One chunk = one wave, one frame at a time over its 64 lanes:
 //   samples -> windowed z[n] = w[2n] x[2n] + i w[2n+1] x[2n+1] (lane j: n = j + 64 r)
 //   -> radix-4 Stockham FFT (Ns = 1, 4, 16, 64; LDS between iterations, natural order out)
 //   -> real-FFT untangle + power (partner bin 256 - k through LDS) -> Slaney bands over each
@@ -645,57 +649,10 @@ __device__ __forceinline__ bool rs_pending(const RsArgs& a) {
            __hip_atomic_load(&a.rs_ctl[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < rs_n_serial(a);
 }
 
-// End of every k_score_f32 workgroup (all modes), after its float32 work: drain the re-score
-// list, count out; the last workgroup out drains the rest, resets the counters for the next
-// launch (ring mode: advances the event watermark) and writes the poll mirror.  Writers
-// publish with a device-scope release before their arrival count: only a workgroup that wrote
-// something the last one reads (a listed segment, a finished slot, or -- with a poll mirror --
-// any score) pays it.  `listed`: lane 0 of a wave that did.
+// The end of a scoring pass (one workgroup, after the list is drained): re-arm the counters
+// for the next launch, advance the event watermark (ring mode) and write the poll mirror.
 template <int RING>
-__device__ void score_tail(const ScoreArgs& a, unsigned char* smem, bool listed, bool drain = true) {
-    int* flag = reinterpret_cast<int*>(smem + L_WG);   // [0] last, [1 + wave] listed, [1 + WAVES] pending
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const RsArgs ra = rs_args(a);
-    bool loaded = false;
-    __syncthreads();   // every wave is done with the float32 tables and scratch
-    if (a.rs_slots && drain) {   // (drain = false: a ring workgroup without a segment, at the start of the tick)
-        if (threadIdx.x == 0) flag[1 + WAVES] = rs_pending(ra);
-        __syncthreads();
-        if (flag[1 + WAVES]) {
-            if (threadIdx.x == 0) EWK_RS_ADD(9, 1);   // workgroups that drain
-            rs_load_tables(a.tab64, smem);
-            __syncthreads();
-            loaded = true;
-            listed = rs_drain<RING>(ra, smem, wave, lane) || listed;
-        }
-    }
-    if (lane == 0) flag[1 + wave] = listed;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int any = 0;
-        for (int w = 0; w < WAVES; ++w) any |= flag[1 + w];
-        if (any) __threadfence();
-        flag[0] = __hip_atomic_fetch_add(&a.rs_ctl[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                  (int)gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!flag[0]) return;
-#ifdef EWK_RS_TIMING
-    const unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
-#endif
-    __threadfence();   // acquire what every other workgroup released before its count
-    if (a.rs_slots) {   // the last workgroup: every other has drained and counted out
-        if (threadIdx.x == 0) flag[1 + WAVES] = rs_pending(ra);
-        __syncthreads();
-        if (flag[1 + WAVES]) {
-            if (!loaded) {
-                rs_load_tables(a.tab64, smem);
-                __syncthreads();
-            }
-            rs_drain<RING>(ra, smem, wave, lane);
-        }
-        __syncthreads();
-    }
+__device__ void tick_end(const ScoreArgs& a) {
     if (threadIdx.x == 0) {
         if (RING) *a.adv_ev_base = *a.n_events;
         *a.work = 0;
@@ -714,9 +671,69 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem, bool listed,
         uint4* dst = reinterpret_cast<uint4*>(a.mirror + 16);
         const int nq = n * (int)(sizeof(ewk_event) / 16);
         // every workgroup that wrote a score released it before its arrival count, and the
-        // fence above (after the last arrival) acquired them for this workgroup
+        // fence after the last arrival acquired them for this workgroup (the scorer's own
+        // scores come from the previous launch)
         for (int i = threadIdx.x; i < nq; i += blockDim.x) dst[i] = src[i];
     }
+}
+
+// Every workgroup of a re-score launch (k_rescore_linear / k_rescore_ring, right after the
+// scorer): drain the list, count out; the last workgroup out drains what is left and ends the
+// pass (tick_end).  A workgroup that finished a slot (wrote a score the poll mirror copies)
+// publishes with a device-scope release before its arrival count.  With nothing listed (most
+// streaming ticks) workgroup 0 ends the pass alone and the others leave at once.
+template <int RING>
+__device__ void score_tail(const ScoreArgs& a, unsigned char* smem) {
+    // [0] last, [1 + wave] finished a slot, [1 + WAVES] pending, [2 + WAVES] slots listed (its own
+    // slot: wave 0 rewrites [1 + WAVES] before the other waves need have read this count)
+    int* flag = reinterpret_cast<int*>(smem + L_WG);
+    static_assert(L_WG + 4 * (3 + WAVES) <= LDS_BYTES, "re-score tail flags");
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const RsArgs ra = rs_args(a);
+    if (threadIdx.x == 0)
+        flag[2 + WAVES] = a.rs_slots ? __hip_atomic_load(&a.rs_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    __syncthreads();
+    if (flag[2 + WAVES] == 0) {   // nothing listed: the list stays empty for this launch
+        if (blockIdx.x == 0) tick_end<RING>(a);
+        return;
+    }
+    bool loaded = false, finished = false;
+    if (threadIdx.x == 0) flag[1 + WAVES] = rs_pending(ra);
+    __syncthreads();
+    if (flag[1 + WAVES]) {
+        if (threadIdx.x == 0) EWK_RS_ADD(9, 1);   // workgroups that drain
+        rs_load_tables(a.tab64, smem);
+        __syncthreads();
+        loaded = true;
+        finished = rs_drain<RING>(ra, smem, wave, lane);
+    }
+    if (lane == 0) flag[1 + wave] = finished;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int any = 0;
+        for (int w = 0; w < WAVES; ++w) any |= flag[1 + w];
+        if (any) __threadfence();
+        flag[0] = __hip_atomic_fetch_add(&a.rs_ctl[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                  (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+#ifdef EWK_RS_TIMING
+    const unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
+#endif
+    __threadfence();   // acquire what every other workgroup released before its count
+    // the last workgroup: every other has drained and counted out
+    if (threadIdx.x == 0) flag[1 + WAVES] = rs_pending(ra);
+    __syncthreads();
+    if (flag[1 + WAVES]) {
+        if (!loaded) {
+            rs_load_tables(a.tab64, smem);
+            __syncthreads();
+        }
+        rs_drain<RING>(ra, smem, wave, lane);
+    }
+    __syncthreads();
+    tick_end<RING>(a);
 #ifdef EWK_RS_TIMING
     if (threadIdx.x == 0) EWK_RS_ADD(13, __builtin_amdgcn_s_memrealtime() - t_last);
 #endif
@@ -727,7 +744,7 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem, bool listed,
 // its register allocation; every workgroup drains, the last one out resets the counters.
 __global__ __launch_bounds__(64 * WAVES, 1) void k_rescore_linear(ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    score_tail<0>(a, smem, false, true);
+    score_tail<0>(a, smem);
 }
 
 // Ring mode (a streaming tick): the same, right after the tick's scorer launch.  Every listed
@@ -738,5 +755,5 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_rescore_linear(ScoreArgs a) {
 template <int RING>
 __global__ __launch_bounds__(64 * WAVES, 1) void k_rescore_ring(ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    score_tail<RING>(a, smem, false, true);
+    score_tail<RING>(a, smem);
 }
