@@ -202,7 +202,18 @@ def host_cores():
     return max(1, min(aff, quota) if quota else aff), aff, quota
 
 
-def cpu_baseline(host_pcm, lengths, offsets, seconds):
+def _rates_summary(res):
+    frames = sum(r[0] for r in res)
+    wall = max(r[2] for r in res)
+    rates = np.array([r[0] / r[2] for r in res if r[2] > 0])   # each worker process's own rate
+    return frames, wall, rates
+
+
+def cpu_baseline(host_pcm, lengths, offsets, seconds, rounds=2):
+    """The oracle port on `procs` pinned worker processes, `rounds` back-to-back rounds of
+    seconds / rounds each in one pool (the first round also warms the workers up): both rounds
+    are reported, `value` is the second's aggregate and `round_agreement_pct` how far the two
+    rounds' median-per-process x cores figures are apart (reproducibility)."""
     import multiprocessing as mp
     procs, aff, quota = host_cores()
     per = max(1, len(lengths) // procs)
@@ -211,26 +222,33 @@ def cpu_baseline(host_pcm, lengths, offsets, seconds):
     for p in range(procs):
         idx = range(p * per, min(len(lengths), (p + 1) * per))
         jobs.append(([host_pcm[offsets[i] - offsets[0]: offsets[i] - offsets[0] + lengths[i]] for i in idx],
-                     seconds, cpus[p]))
+                     seconds / rounds, cpus[p]))
     ctx = mp.get_context("spawn")
+    out_rounds = []
     with ctx.Pool(procs, initializer=_pool_init) as pool:
-        res = pool.map(_cpu_worker, jobs, chunksize=1)
-    frames = sum(r[0] for r in res)
-    segs = sum(r[1] for r in res)
-    wall = max(r[2] for r in res)
-    rates = np.array([r[0] / r[2] for r in res if r[2] > 0])   # each worker process's own rate
-    return {"value": frames / wall, "unit": "frames/s", "cores": procs, "host_cores_affinity": aff,
+        for _ in range(rounds):
+            res = pool.map(_cpu_worker, jobs, chunksize=1)
+            frames, wall, rates = _rates_summary(res)
+            out_rounds.append({"value": frames / wall, "median_x_cores": float(np.median(rates) * procs),
+                               "segments": sum(r[1] for r in res), "frames": frames, "rates": rates})
+    last = out_rounds[-1]
+    rates = last["rates"]
+    mx = [r["median_x_cores"] for r in out_rounds]
+    return {"value": last["value"], "unit": "frames/s", "cores": procs, "host_cores_affinity": aff,
             "cpu_quota_cores": quota, "kind": "port", "pinned": cpus[0] is not None,
             # robust to one slow or one unusually idle core: the median process rate x cores
-            "median_x_cores": float(np.median(rates) * procs),
+            "median_x_cores": last["median_x_cores"],
+            "rounds": [{"value": r["value"], "median_x_cores": r["median_x_cores"]} for r in out_rounds],
+            "round_agreement_pct": float(100.0 * (max(mx) - min(mx)) / max(1e-9, float(np.mean(mx)))),
             # per-core rate and its spread over the worker processes: the aggregate depends on
             # how many cores the box's cgroup grants and how busy its other tenants keep them
             "per_core": {"median": float(np.median(rates)), "min": float(rates.min()), "max": float(rates.max()),
                          "spread_pct": float(100.0 * (rates.max() - rates.min()) / np.median(rates)),
                          "unit": "frames/s per process"},
-            "sample": f"{segs} segments ({frames} MFCC frames) of the same ragged batch, float64 candidate path, "
-                      f"oracle/mfcc_ref.py (numpy/scipy restatement of librosa 0.11.0 mfcc + scipy cosine), "
-                      f"{procs} processes x ~{seconds:.0f} s, OMP_NUM_THREADS=1"}
+            "sample": f"{last['segments']} segments ({last['frames']} MFCC frames) of the same ragged batch per round, "
+                      f"float64 candidate path, oracle/mfcc_ref.py (numpy/scipy restatement of librosa 0.11.0 mfcc + "
+                      f"scipy cosine), {procs} pinned processes x {rounds} rounds x ~{seconds / rounds:.0f} s, "
+                      f"OMP_NUM_THREADS=1"}
 
 
 def event_sources(word, rng):

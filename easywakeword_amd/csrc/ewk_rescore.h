@@ -428,10 +428,15 @@ __device__ void rs_finish(const RsArgs& a, RsSlot* sp, int seg, int T, float the
     int fl = 0;
     RsAcc acc;
     double pv[7];
-    if (parts) {
-        for (int c = 0; c < nch; ++c) {
-            mx = fmax(mx, parts[c].mx);
-            fl |= parts[c].flags;
+    if (parts) {   // lane c reads chunk c's max and flags: one memory round trip per 64 chunks
+        for (int c0 = 0; c0 < nch; c0 += 64) {
+            double m = -INFINITY;
+            int f = 0;
+            if (c0 + lane < nch) { m = parts[c0 + lane].mx; f = parts[c0 + lane].flags; }
+            mx = fmax(mx, wave_max_d(m));
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) f |= __shfl_xor(f, o, 64);
+            fl |= f;
         }
     } else {   // serial: a first pass with theta_s, merged as it goes
         for (int c = 0; c < nch; ++c) {
@@ -449,19 +454,32 @@ __device__ void rs_finish(const RsArgs& a, RsSlot* sp, int seg, int T, float the
     if (lane == 0 && parts) { EWK_RS_ADD(6, redo_all); EWK_RS_ADD(7, nch); }
     if (!nan_in && (parts || redo_all || (fl & 1))) {
         if (!parts) acc = RsAcc();
+        // the part records are read one chunk ahead of their merge (uncached memory: a round
+        // trip each), in chunk order
+        double nx[7];
+        int nn = 0, nfl = 0;
+        auto fetch = [&](int c) {
+            if (parts && c < nch) {
+                nn = parts[c].n;
+                nfl = parts[c].flags;
+                if (lane < NMFCC) {
+#pragma unroll
+                    for (int q = 0; q < 7; ++q) nx[q] = parts[c].v[q * NMFCC + lane];
+                }
+            }
+        };
+        fetch(0);
         for (int c = 0; c < nch; ++c) {
-            int n;
-            if (!parts || redo_all || (parts[c].flags & 1)) {   // classification at the exact theta
+            int n = nn;
+            const int cfl = nfl;
+#pragma unroll
+            for (int q = 0; q < 7; ++q) pv[q] = nx[q];
+            fetch(c + 1);
+            if (!parts || redo_all || (cfl & 1)) {   // classification at the exact theta
                 double m;
                 int f;
                 if (lane == 0 && parts) EWK_RS_ADD(8, 1);
                 rs_chunk(v, T, c, theta, -1.0, cl, smem, wbuf, lane, pv, m, n, f);
-            } else {
-                n = parts[c].n;
-                if (lane < NMFCC) {
-#pragma unroll
-                    for (int q = 0; q < 7; ++q) pv[q] = parts[c].v[q * NMFCC + lane];
-                }
             }
             rs_merge(acc, pv, n);
         }
