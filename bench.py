@@ -69,7 +69,7 @@ def parse():
     ap.add_argument("--stream-ticks", type=int, default=600, help="ticks after the 10 s prefill")
     ap.add_argument("--big-streams", type=int, default=131072,
                     help="north-star run: streams resident with the reference's full 10 s rings (0 = skip)")
-    ap.add_argument("--max-streams", type=int, default=2097152,
+    ap.add_argument("--max-streams", type=int, default=1 << 23,
                     help="streams resident with compact int16 sample rings, capped by free HBM (0 = skip)")
     ap.add_argument("--max-ring", type=int, default=48000, help="compact ring samples per stream (3 s)")
     ap.add_argument("--max-float32", action="store_true",

@@ -44,3 +44,10 @@ if [ "$MODE" = bench ]; then   # the default bench line, then its rocprofv3 kern
   head -12 "$R/gpurun_out/${TAG}_kernel_stats.txt"; tail -3 "$R/gpurun_out/${TAG}_kernel_stats.txt"
   exit $rc
 fi
+if [ "$MODE" = maxstreams ]; then   # the streaming_max leg alone at the default request (HBM-capped)
+  timeout -k 10 600 python bench.py --steps 3 --warmup 2 --no-cpu-baseline --fixed-len 0 --short-len 0 \
+     --confirm-batch 0 --no-host-ingest --big-streams 0 --stream-ticks 100 > gpurun_out/${TAG}_cur.log 2>&1
+  rc=$?; cp gpurun_out/${TAG}_cur.log gpurun_out/${TAG}_maxstreams.log; echo "maxstreams rc=$rc"
+  python scripts/stream_line.py gpurun_out/${TAG}_maxstreams.log || tail -c 3000 gpurun_out/${TAG}_maxstreams.log
+  exit $rc
+fi
