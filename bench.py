@@ -211,8 +211,8 @@ def _rates_summary(res):
 
 def cpu_baseline(host_pcm, lengths, offsets, seconds, rounds=2):
     """The oracle port on `procs` pinned worker processes, `rounds` back-to-back rounds of
-    seconds / rounds each in one pool (the first round also warms the workers up): both rounds
-    are reported, `value` is the second's aggregate and `round_agreement_pct` how far the two
+    seconds / rounds each in one pool after a short warm-up round: both rounds are reported,
+    `value` is the second's aggregate and `round_agreement_pct` how far the two
     rounds' median-per-process x cores figures are apart (reproducibility)."""
     import multiprocessing as mp
     procs, aff, quota = host_cores()
@@ -226,6 +226,9 @@ def cpu_baseline(host_pcm, lengths, offsets, seconds, rounds=2):
     ctx = mp.get_context("spawn")
     out_rounds = []
     with ctx.Pool(procs, initializer=_pool_init) as pool:
+        # an unreported ~1 s warm-up round first (imports, first-call and page-fault costs,
+        # clock ramp: a first timed round ran 25 % below the second on one box)
+        pool.map(_cpu_worker, [(j[0], 1.0, j[2]) for j in jobs], chunksize=1)
         for _ in range(rounds):
             res = pool.map(_cpu_worker, jobs, chunksize=1)
             frames, wall, rates = _rates_summary(res)
