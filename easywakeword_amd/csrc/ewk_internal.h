@@ -68,6 +68,7 @@ void build_tables64(Tables64* t);
 // every slot of ewk_score_segments_f64) is serial: one wave runs its chunks in order.
 constexpr int kRsFrames = 8;   // frames per re-score chunk
 constexpr int kRsCtl = 8;      // ints of ScoreArgs::rs_ctl
+constexpr int kRsMelW = 12;    // widest Slaney band of the basis in bins (fp64 mel window; checked at engine creation)
 struct RsSlot {
     int32_t seg;       // segment (linear) or event (ring) index
     int32_t T;         // frames

@@ -282,12 +282,30 @@ __device__ __forceinline__ void rs_frame(const float (&smp)[8], const RsLane& c,
     const float* mw = reinterpret_cast<const float*>(smem + RS_MW);
     double* xa = reinterpret_cast<double*>(wbuf + RS_XA);
     float* xb = reinterpret_cast<float*>(wbuf + RS_XB);
+    // both bands' weights and powers are requested together (a fixed kRsMelW-wide window,
+    // predicated: the loads of a dynamic-trip loop each waited a full LDS round trip); the
+    // accumulation order is the band's bin order, as before
+    double pw[2][kRsMelW];
+    float ww[2][kRsMelW];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int m = h ? NMEL - 1 - lane : lane;
-        const int lo = mlo[m], o0 = moff[m], o1 = moff[m + 1];
+        const int lo = mlo[m], o0 = moff[m], nw = moff[m + 1] - o0;
+#pragma unroll
+        for (int q = 0; q < kRsMelW; ++q) {
+            const bool in = q < nw;
+            ww[h][q] = in ? mw[o0 + q] : 0.0f;
+            pw[h][q] = in ? P[lo + q] : 0.0;
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int m = h ? NMEL - 1 - lane : lane;
+        const int nw = moff[m + 1] - moff[m];
         double acc = 0.0;
-        for (int o = o0; o < o1; ++o) acc = fma((double)mw[o], P[lo + o - o0], acc);
+#pragma unroll
+        for (int q = 0; q < kRsMelW; ++q)
+            if (q < nw) acc = fma((double)ww[h][q], pw[h][q], acc);
         const double db = 10.0 * log10(acc < 1e-10 ? 1e-10 : acc);   // np.maximum: NaN propagates
         const bool keep = db >= theta_s;
         xa[m * kRsFrames + f] = keep ? db : 0.0;

@@ -51,3 +51,10 @@ if [ "$MODE" = maxstreams ]; then   # the streaming_max leg alone at the default
   python scripts/stream_line.py gpurun_out/${TAG}_maxstreams.log || tail -c 3000 gpurun_out/${TAG}_maxstreams.log
   exit $rc
 fi
+if [ "$MODE" = n2 ]; then   # the bench's N > 1 path rehearsed with 2 gloo ranks on the one GPU
+  EWK_BENCH_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 \
+     --master-addr 127.0.0.1 --master-port 29613 bench.py --gpus 2 --steps 5 --warmup 2 --big-streams 0 --big-ticks 100 \
+     --max-streams 262144 --no-host-ingest --confirm-batch 0 --fixed-len 0 --short-len 0 > gpurun_out/${TAG}_cur.log 2>&1
+  rc=$?; cp gpurun_out/${TAG}_cur.log gpurun_out/${TAG}_n2.log; echo "n2 rc=$rc"; grep "^{" gpurun_out/${TAG}_n2.log | tail -1 | head -c 1500
+  exit $rc
+fi
