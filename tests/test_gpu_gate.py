@@ -111,7 +111,7 @@ def test_many_streams_vs_oracle(template):
 
 def test_ring_tick_fp64_rescore_in_last_workgroup(template):
     """rescore_margin = 1e9: every ring segment is queued for the fp64 re-score, which the
-    last k_score_f32 workgroup of the tick runs (no separate launch): all events carry
+    tick's re-score launch (k_rescore_ring, right after the scorer) drains: all events carry
     EWK_EV_RESCORED and the float64 reference score within 1e-9, over several ticks per
     push and several pushes (the watermark advances in the same tick end)."""
     gate = dict(pre_speech_silence=0.8, speech_duration_min=0.3, speech_duration_max=2.0, post_speech_silence=0.4)
