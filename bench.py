@@ -209,10 +209,11 @@ def _rates_summary(res):
     return frames, wall, rates
 
 
-def cpu_baseline(host_pcm, lengths, offsets, seconds, rounds=2):
+def cpu_baseline(host_pcm, lengths, offsets, seconds, rounds=3):
     """The oracle port on `procs` pinned worker processes, `rounds` back-to-back rounds of
-    seconds / rounds each in one pool after a short warm-up round: both rounds are reported,
-    `value` is the second's aggregate and `round_agreement_pct` how far the two
+    seconds / rounds each in one pool after a short warm-up round.  Every round is reported;
+    `value` is the best round's aggregate (the box's other tenants only ever slow a round down:
+    two rounds on one box differed by 35 % in round 4) and `round_agreement_pct` how far the
     rounds' median-per-process x cores figures are apart (reproducibility)."""
     import multiprocessing as mp
     procs, aff, quota = host_cores()
@@ -234,11 +235,12 @@ def cpu_baseline(host_pcm, lengths, offsets, seconds, rounds=2):
             frames, wall, rates = _rates_summary(res)
             out_rounds.append({"value": frames / wall, "median_x_cores": float(np.median(rates) * procs),
                                "segments": sum(r[1] for r in res), "frames": frames, "rates": rates})
-    last = out_rounds[-1]
+    last = max(out_rounds, key=lambda r: r["value"])   # the best round
     rates = last["rates"]
     mx = [r["median_x_cores"] for r in out_rounds]
     return {"value": last["value"], "unit": "frames/s", "cores": procs, "host_cores_affinity": aff,
             "cpu_quota_cores": quota, "kind": "port", "pinned": cpus[0] is not None,
+            "statistic": f"best of {rounds} rounds",
             # robust to one slow or one unusually idle core: the median process rate x cores
             "median_x_cores": last["median_x_cores"],
             "rounds": [{"value": r["value"], "median_x_cores": r["median_x_cores"]} for r in out_rounds],
