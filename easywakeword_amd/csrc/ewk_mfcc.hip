@@ -1504,7 +1504,7 @@ __device__ __forceinline__ double score_f32_finish(float uu_m, float uu_s, float
 // pipeline cannot decide it alone.  theta_s: the float32 pass's log-mel max - 80 dB.
 template <int RING>
 __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, float csf, float tmf, float tsf,
-                                               int lane, int seg, int len, float theta_s, bool& listed) {
+                                               int lane, int seg, int len, float theta_s) {
     bool near = a.list_all;
     if (a.has_template) {
         double score, std2, mean2;
@@ -1539,17 +1539,13 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, fl
             if (RING) {
                 a.events[seg].score = score;
                 a.events[seg].match = match;
-                if (a.mirror) listed = true;   // the last workgroup copies this event to the poll mirror
             } else {
                 a.out_score[seg] = score;
                 if (a.out_match) a.out_match[seg] = (uint8_t)match;
             }
         }
     }
-    if (lane == 0 && near && a.rs_slots) {
-        rs_list(a, seg, len, theta_s);
-        listed = true;   // (lane 0) this wave listed a segment for the fp64 re-score
-    }
+    if (lane == 0 && near && a.rs_slots) rs_list(a, seg, len, theta_s);   // drained by the re-score launch
 }
 
 
@@ -1651,7 +1647,6 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
     // the template is loop-invariant: fetched once, off every segment's critical path.
     // (Reserving the next work item ahead was tried: the tail imbalance costs more.)
     const bool act = lane < NMFCC;
-    bool listed = false;   // lane 0: this wave listed a segment for the fp64 re-score (score_tail)
     const float tmf = (a.has_template && act) ? a.tmpl[lane] : 0.0f;
     const float tsf = (a.has_template && act) ? a.tmpl[NMFCC + lane] : 0.0f;
     // Ring mode, MODE 1 (a tick of ~10^3-10^4 streams: a few hundred segments, latency
@@ -1678,7 +1673,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
                 segment_stats_coop(v, smem, scr, tile, spec, wave, lane, lo, misc0, theta_s);
                 if (wave == 0 && (a.has_template || a.list_all))
                     score_epilogue<RING>(a, act ? misc0[lane] : 0.0f, act ? misc0[20 + lane] : 0.0f, tmf, tsf, lane,
-                                         seg, v.len, theta_s, listed);
+                                         seg, v.len, theta_s);
             }
             if (threadIdx.x == 0) wg_idx[0] = nxt;
             __syncthreads();
@@ -1725,7 +1720,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
             if (a.out_mean) a.out_mean[(int64_t)seg * NMFCC + lane] = cmf;
             if (a.out_std) a.out_std[(int64_t)seg * NMFCC + lane] = csf;
         }
-        if (a.has_template || a.list_all) score_epilogue<RING>(a, cmf, csf, tmf, tsf, lane, seg, v.len, theta_s, listed);
+        if (a.has_template || a.list_all) score_epilogue<RING>(a, cmf, csf, tmf, tsf, lane, seg, v.len, theta_s);
         lds_order();
         EWK_TS(tw3);
         EWK_TADD(7, tw2, tw3);
@@ -1738,7 +1733,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
     if (lane == 0)
         for (int k = 0; k < kDbgN; ++k) atomicAdd(&g_ewk_dbg[k], (unsigned long long)dbg[k]);
 #endif
-    (void)listed;   // the list is drained by k_rescore_linear / k_rescore_ring, launched after this kernel
+    // (the fp64 list is drained by k_rescore_linear / k_rescore_ring, launched after this kernel)
 }
 
 #ifdef EWK_RS_TIMING

@@ -317,3 +317,27 @@ def test_non_finite_samples_do_not_disturb_the_batch(engine):
         cm, cs = mfcc_ref.extract_mfcc(x.astype(np.float64))
         ref = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
         assert score_close(score[i], ref, SCORE_TOL), (i, score[i], ref)
+
+
+def test_every_segment_rescored_part_pool_overflow():
+    """rescore_margin = 1e9 lists every segment of a 1,500-segment batch for the fp64 re-score:
+    ~24,000 8-frame chunks against the engine's 16,384 part records, so the slots listed after
+    the pool runs out go serial (one wave each, claimed from their own list after every chunk
+    is taken).  Every score must equal the fp64 API's (ewk_score_segments_f64, every slot
+    serial) within 1e-9, and every decision must follow it."""
+    from easywakeword_amd import Engine
+    segs = synth.ragged_segments(2024, 1500, 6400, 40000)
+    e = Engine(rescore_margin=1e9)
+    f = Engine()
+    try:
+        e.template_from_pcm(synth.load_word())
+        f.template_from_pcm(synth.load_word())
+        _, _, s64 = f.score_f64(segs)
+        _, _, sc, mt = e.score(segs, candidate_dtype="float64")
+        ok = np.isfinite(s64)
+        assert np.array_equal(np.isnan(sc), np.isnan(s64))
+        assert float(np.max(np.abs(sc[ok] - s64[ok]))) <= 1e-9
+        assert np.array_equal(mt.astype(bool)[ok], s64[ok] >= 75.0)
+    finally:
+        e.close()
+        f.close()
