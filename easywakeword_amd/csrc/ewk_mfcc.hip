@@ -1883,7 +1883,7 @@ hipError_t launch_score_f32(const Tables* d_tab, const ScoreArgs& a, int ring_mo
 
 hipError_t launch_rescore_linear(const ScoreArgs& a, hipStream_t s) {
     if (a.n_seg <= 0 || !a.rs_slots) return hipSuccess;
-    hipLaunchKernelGGL(k_rescore_linear, dim3(kScoreGridMax), dim3(64 * WAVES), LDS_BYTES, s, a);
+    hipLaunchKernelGGL(k_rescore_linear, dim3(kScoreGridMax), dim3(64 * RS_NW), RS_LDS, s, a);
     return hipGetLastError();
 }
 
@@ -1891,8 +1891,8 @@ hipError_t launch_rescore_linear(const ScoreArgs& a, hipStream_t s) {
 // counters and advances the watermark).
 hipError_t launch_rescore_ring(const ScoreArgs& a, hipStream_t s) {
     if (a.n_seg <= 0) return hipSuccess;
-    if (a.pcm16) hipLaunchKernelGGL(k_rescore_ring<2>, dim3(kScoreGridRing), dim3(64 * WAVES), LDS_BYTES, s, a);
-    else hipLaunchKernelGGL(k_rescore_ring<1>, dim3(kScoreGridRing), dim3(64 * WAVES), LDS_BYTES, s, a);
+    if (a.pcm16) hipLaunchKernelGGL(k_rescore_ring<2>, dim3(kScoreGridRing), dim3(64 * RS_NW), RS_LDS, s, a);
+    else hipLaunchKernelGGL(k_rescore_ring<1>, dim3(kScoreGridRing), dim3(64 * RS_NW), RS_LDS, s, a);
     return hipGetLastError();
 }
 

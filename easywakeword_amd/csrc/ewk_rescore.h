@@ -83,17 +83,27 @@ __device__ __forceinline__ RsArgs rs_args(const ScoreArgs& a) {
     return r;
 }
 
-// LDS of the re-score (the float32 tables and scratch are dead by then; ends below L_WG)
-constexpr int RS_D = 0;                                     // double [NMEL][NMFCC]
-constexpr int RS_MLO = RS_D + NMEL * NMFCC * 8;             // int [NMEL]
+// The re-score launches run their own workgroup shape: RS_NW waves sharing the tables below.
+// Two waves per SIMD: a third (12 waves, <= 168 VGPRs) made each chunk 1.85x slower -- the
+// SIMD's fp64 VALU is the shared resource, not latency (profiles/r04_v9_rescore_variants.txt).
+#ifndef EWK_RS_NW
+#define EWK_RS_NW 8
+#endif
+constexpr int RS_NW = EWK_RS_NW;
+// LDS of the re-score launch.  The DCT table keeps bands 0..63 only: the DCT-II rows are
+// (anti)symmetric, D[k][127 - m] = (-1)^k D[k][m] (the fp64 table is built that way, exactly).
+constexpr int RS_D = 0;                                     // double [NMEL / 2][NMFCC]
+constexpr int RS_MLO = RS_D + (NMEL / 2) * NMFCC * 8;       // int [NMEL]
 constexpr int RS_MOFF = RS_MLO + NMEL * 4;                  // int [NMEL + 1]
 constexpr int RS_MW = RS_MOFF + (NMEL + 4) * 4;             // float [2 NBIN + 2 NMEL]
-constexpr int RS_WAVES = (RS_MW + (2 * NBIN + 2 * NMEL) * 4 + 15) & ~15;
+constexpr int RS_MW_N = 2 * NBIN + 2 * NMEL;
+constexpr int RS_WAVES = (RS_MW + RS_MW_N * 4 + 15) & ~15;
 constexpr int RS_BUF = 0;                                   // per wave: double2 [256] FFT / double P[257]
-constexpr int RS_XA = 256 * 16;                             // double [NMEL][kRsFrames]: x or 0 (clamped)
-constexpr int RS_XB = RS_XA + NMEL * kRsFrames * 8;         // float [NMEL][kRsFrames]: 0 or 1 (clamped)
-constexpr int RS_WAVE_BYTES = RS_XB + NMEL * kRsFrames * 4;
-static_assert(RS_WAVES + WAVES * RS_WAVE_BYTES <= L_WG, "the re-score carve must end below the workgroup flags");
+constexpr int RS_XA = 256 * 16;                             // double [NMEL][kRsFrames]: the chunk's log-mel
+constexpr int RS_WAVE_BYTES = RS_XA + NMEL * kRsFrames * 8;
+constexpr int RS_FLAGS = RS_WAVES + RS_NW * RS_WAVE_BYTES;  // int [3 + RS_NW]: score_tail's flags
+constexpr int RS_LDS = RS_FLAGS + 4 * (3 + RS_NW);
+static_assert(RS_LDS <= 160 * 1024, "the re-score workgroup must fit a CU's LDS");
 static_assert(NMFCC == 20 && kRsFrames == 8, "the DCT lane split assumes 20 coefficients and 8-frame chunks");
 
 // Between a wave's LDS writes and its other lanes' reads: LDS operations of one wave execute in
@@ -170,7 +180,7 @@ __device__ void rs_load_tables(const Tables64* __restrict__ tb, unsigned char* s
     int* mlo = reinterpret_cast<int*>(smem + RS_MLO);
     int* moff = reinterpret_cast<int*>(smem + RS_MOFF);
     float* mw = reinterpret_cast<float*>(smem + RS_MW);
-    for (int i = threadIdx.x; i < NMEL * NMFCC; i += blockDim.x) {
+    for (int i = threadIdx.x; i < (NMEL / 2) * NMFCC; i += blockDim.x) {
         const int m = i / NMFCC, k = i % NMFCC;
         D[i] = tb->dct[k * NMEL + m];
     }
@@ -224,17 +234,27 @@ __device__ __forceinline__ void rs_load(const RsSrc<RING>& v, int t, int lane, f
     }
 }
 
-__device__ __forceinline__ void rs_frame(const float (&smp)[8], const RsLane& c, unsigned char* wbuf,
+// The windowed frame z[n] = w[2n] x[2n] + i w[2n+1] x[2n+1], n = lane + 64 r.
+__device__ __forceinline__ void rs_window(const float (&smp)[8], const RsLane& c, double2 (&x)[4]) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[r] = make_double2(c.win[2 * r] * (double)smp[2 * r], c.win[2 * r + 1] * (double)smp[2 * r + 1]);
+}
+
+__device__ __forceinline__ void rs_frame(const double2 (&xw)[4], const RsLane& c, unsigned char* wbuf,
                                          const unsigned char* smem, int lane, int f, double theta_s, double W,
-                                         double& mx, bool& amb, bool& nanf) {
+                                         double& mx, bool& amb, bool& nanf, bool& clp) {
     double2* buf = reinterpret_cast<double2*>(wbuf + RS_BUF);
     double2 x[4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) x[r] = make_double2(c.win[2 * r] * (double)smp[2 * r], c.win[2 * r + 1] * (double)smp[2 * r + 1]);
+    for (int r = 0; r < 4; ++r) x[r] = xw[r];
     // radix-4 Stockham autosort: v[r] = d[j + 64 r], v[r] *= W_{4 Ns}^{r (j % Ns)}, DFT4,
     // V[r] -> d'[(j / Ns) 4 Ns + j % Ns + r Ns]; natural order after Ns = 64
 #pragma unroll
+#ifndef EWK_RS_SKIP_FFT
     for (int it = 0; it < 4; ++it) {
+#else
+    for (int it = 0; it < 4; it += 3) {
+#endif
         if (it > 0) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) x[r] = buf[lane + 64 * r];
@@ -281,35 +301,39 @@ __device__ __forceinline__ void rs_frame(const float (&smp)[8], const RsLane& c,
     const int* moff = reinterpret_cast<const int*>(smem + RS_MOFF);
     const float* mw = reinterpret_cast<const float*>(smem + RS_MW);
     double* xa = reinterpret_cast<double*>(wbuf + RS_XA);
-    float* xb = reinterpret_cast<float*>(wbuf + RS_XB);
-    // both bands' weights and powers are requested together (a fixed kRsMelW-wide window,
-    // predicated: the loads of a dynamic-trip loop each waited a full LDS round trip); the
-    // accumulation order is the band's bin order, as before
-    double pw[2][kRsMelW];
-    float ww[2][kRsMelW];
+    // a fixed kRsMelW-wide window per band, read unconditionally (one LDS round trip, no
+    // branch); past the band's support the weight and the power are selected to 0, and
+    // fma(0, 0, acc) = acc, so the sum is the band's, in bin order
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int m = h ? NMEL - 1 - lane : lane;
         const int lo = mlo[m], o0 = moff[m], nw = moff[m + 1] - o0;
+        double pw[kRsMelW];
+        float ww[kRsMelW];
 #pragma unroll
         for (int q = 0; q < kRsMelW; ++q) {
-            const bool in = q < nw;
-            ww[h][q] = in ? mw[o0 + q] : 0.0f;
-            pw[h][q] = in ? P[lo + q] : 0.0;
+            ww[q] = q < nw ? mw[min(o0 + q, RS_MW_N - 1)] : 0.0f;
+            pw[q] = P[lo + q];   // lo + q < 2 * 256: inside the wave's FFT buffer
         }
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int m = h ? NMEL - 1 - lane : lane;
-        const int nw = moff[m + 1] - moff[m];
         double acc = 0.0;
+#ifndef EWK_RS_SKIP_MEL
+        // past the band: weight 0 times a finite power of this frame (its FFT buffer; a NaN
+        // there means NaN samples, and then every bin is NaN) adds +-0, and acc + -0 = acc
 #pragma unroll
-        for (int q = 0; q < kRsMelW; ++q)
-            if (q < nw) acc = fma((double)ww[h][q], pw[h][q], acc);
+        for (int q = 0; q < kRsMelW; ++q) acc = fma((double)ww[q], pw[q], acc);
+#else   // (timing experiment: one bin per band)
+        acc = pw[0] + (double)ww[0] + (double)nw;
+#endif
+#ifndef EWK_RS_SKIP_LOG
         const double db = 10.0 * log10(acc < 1e-10 ? 1e-10 : acc);   // np.maximum: NaN propagates
-        const bool keep = db >= theta_s;
-        xa[m * kRsFrames + f] = keep ? db : 0.0;
-        xb[m * kRsFrames + f] = keep ? 0.0f : 1.0f;
+#else
+        const double db = acc;
+#endif
+        // the A operand, or -0.0 for a value the clamp replaces (NaN included): fma(d, -0, A) = A
+        // as with +0, and db is never -0.0 (10 log10(acc), acc >= 1e-10), so -0.0 also marks
+        // the B operand for rs_dct (no second tile)
+        xa[m * kRsFrames + f] = db >= theta_s ? db : -0.0;
+        clp = clp || !(db >= theta_s);
         mx = fmax(mx, db);
         amb = amb || fabs(db - theta_s) <= W;
         nanf = nanf || db != db;
@@ -317,31 +341,46 @@ __device__ __forceinline__ void rs_frame(const float (&smp)[8], const RsLane& c,
     wave_sync();
 }
 
-// DCT of the chunk's n frames split at theta_s: lane k < 20 returns A_k, B_k of frames 0..7.
-// Lanes (k, h) = (l % 20, l / 20), l < 60, take bands [43 h, 43 h + 43); the thirds are
-// added in a fixed order (h = 0, 1, 2).
-__device__ __forceinline__ void rs_dct(const unsigned char* smem, unsigned char* wbuf, int lane, double (&A)[8],
-                                       double (&B)[8]) {
+// DCT of the chunk's n frames split at theta_s: lane k < 20 returns A_k, B_k of frames 0..7
+// (A: the values x >= theta_s, B: the weights of the others -- NaN included -- which the
+// clamp replaces by theta; rs_frame stored those as -0.0).  Lanes (k, h) = (l % 20, l / 20),
+// l < 60, take bands [43 h, 43 h + 43), the next band's reads issued before this band's FMAs;
+// the thirds are added in a fixed order (h = 0, 1, 2).
+__device__ __forceinline__ void rs_dct(const unsigned char* smem, unsigned char* wbuf, int lane, bool need_b,
+                                       double (&A)[8], double (&B)[8]) {
     const double* D = reinterpret_cast<const double*>(smem + RS_D);
     double* xa = reinterpret_cast<double*>(wbuf + RS_XA);
-    const float* xb = reinterpret_cast<const float*>(wbuf + RS_XB);
 #pragma unroll
     for (int f = 0; f < 8; ++f) { A[f] = 0.0; B[f] = 0.0; }
     if (lane < 60) {
         const int k = lane % NMFCC, h = lane / NMFCC;
-        const int m0 = 43 * h, m1 = min(NMEL, m0 + 43);
+        const int m0 = 43 * h;
+#ifndef EWK_RS_SKIP_DCT
+        const int m1 = min(NMEL, m0 + 43);
+#else
+        const int m1 = m0 + 1;
+#endif
+        // D[k][m] = (-1)^k D[k][127 - m]: the sign is applied at use, after the load's wait
+        auto draw = [&](int m) { return D[(m >= NMEL / 2 ? NMEL - 1 - m : m) * NMFCC + k]; };
+        double dn = draw(m0);
+        double4 n0 = reinterpret_cast<const double4*>(xa + m0 * kRsFrames)[0];
+        double4 n1 = reinterpret_cast<const double4*>(xa + m0 * kRsFrames)[1];
         for (int m = m0; m < m1; ++m) {
-            const double d = D[m * NMFCC + k];
-            const double4* pa = reinterpret_cast<const double4*>(xa + m * kRsFrames);
-            const float4* pb = reinterpret_cast<const float4*>(xb + m * kRsFrames);
-            const double4 a0 = pa[0], a1 = pa[1];
-            const float4 b0 = pb[0], b1 = pb[1];
-            const double av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-            const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+            const double d = m >= NMEL / 2 && (k & 1) ? -dn : dn;
+            const double av[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
+            if (m + 1 < m1) {
+                dn = draw(m + 1);
+                n0 = reinterpret_cast<const double4*>(xa + (m + 1) * kRsFrames)[0];
+                n1 = reinterpret_cast<const double4*>(xa + (m + 1) * kRsFrames)[1];
+            }
 #pragma unroll
-            for (int f = 0; f < 8; ++f) {
-                A[f] = fma(d, av[f], A[f]);
-                B[f] = fma(d, (double)bv[f], B[f]);
+            for (int f = 0; f < 8; ++f) A[f] = fma(d, av[f], A[f]);
+            if (need_b) {   // (wave-uniform: a chunk with no clamped value has B = 0 exactly)
+#pragma unroll
+                for (int f = 0; f < 8; ++f) {
+                    const bool clamped = __double2hiint(av[f]) == (int)0x80000000;   // -0.0
+                    B[f] = fma(d, clamped ? 1.0 : 0.0, B[f]);
+                }
             }
         }
     }
@@ -379,17 +418,23 @@ __device__ void rs_chunk(const RsSrc<RING>& v, int T, int c, double theta_s, dou
     const int t0 = c * kRsFrames;
     n = min(kRsFrames, T - t0);
     double m = -INFINITY;
-    bool amb = false, nanf = false;
-    float cur[8], nxt[8];
-    rs_load(v, t0, lane, cur);
+    bool amb = false, nanf = false, clp = false;
+    float smp[8];
+    rs_load(v, t0, lane, smp);
     for (int f = 0; f < n; ++f) {
-        if (f + 1 < n) rs_load(v, t0 + f + 1, lane, nxt);
-        rs_frame(cur, cl, wbuf, smem, lane, f, theta_s, W, m, amb, nanf);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) cur[i] = nxt[i];
+        double2 xw[4];
+        rs_window(smp, cl, xw);
+        // the next frame's loads go out only after this frame's samples are consumed (issued
+        // before, the compiler's in-order vmcnt wait for this frame's samples also covered the
+        // first of them; time-neutral, profiles/r04_v9_rescore_pmc.txt)
+        asm volatile("" ::"v"(xw[0].x), "v"(xw[0].y), "v"(xw[1].x), "v"(xw[1].y), "v"(xw[2].x), "v"(xw[2].y),
+                     "v"(xw[3].x), "v"(xw[3].y)
+                     : "memory");
+        if (f + 1 < n) rs_load(v, t0 + f + 1, lane, smp);
+        rs_frame(xw, cl, wbuf, smem, lane, f, theta_s, W, m, amb, nanf, clp);
     }
     double A[8], B[8];
-    rs_dct(smem, wbuf, lane, A, B);
+    rs_dct(smem, wbuf, lane, __ballot(clp) != 0, A, B);
     const double rA = A[0], rB = B[0];
     double sA = 0.0, sB = 0.0, sAA = 0.0, sAB = 0.0, sBB = 0.0;
 #pragma unroll
@@ -720,23 +765,22 @@ __device__ void tick_end(const ScoreArgs& a) {
 // streaming ticks) workgroup 0 ends the pass alone and the others leave at once.
 template <int RING>
 __device__ void score_tail(const ScoreArgs& a, unsigned char* smem) {
-    // [0] last, [1 + wave] finished a slot, [1 + WAVES] pending, [2 + WAVES] slots listed (its own
-    // slot: wave 0 rewrites [1 + WAVES] before the other waves need have read this count)
-    int* flag = reinterpret_cast<int*>(smem + L_WG);
-    static_assert(L_WG + 4 * (3 + WAVES) <= LDS_BYTES, "re-score tail flags");
+    // [0] last, [1 + wave] finished a slot, [1 + RS_NW] pending, [2 + RS_NW] slots listed (its own
+    // slot: wave 0 rewrites [1 + RS_NW] before the other waves need have read this count)
+    int* flag = reinterpret_cast<int*>(smem + RS_FLAGS);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const RsArgs ra = rs_args(a);
     if (threadIdx.x == 0)
-        flag[2 + WAVES] = a.rs_slots ? __hip_atomic_load(&a.rs_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        flag[2 + RS_NW] = a.rs_slots ? __hip_atomic_load(&a.rs_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
     __syncthreads();
-    if (flag[2 + WAVES] == 0) {   // nothing listed: the list stays empty for this launch
+    if (flag[2 + RS_NW] == 0) {   // nothing listed: the list stays empty for this launch
         if (blockIdx.x == 0) tick_end<RING>(a);
         return;
     }
     bool loaded = false, finished = false;
-    if (threadIdx.x == 0) flag[1 + WAVES] = rs_pending(ra);
+    if (threadIdx.x == 0) flag[1 + RS_NW] = rs_pending(ra);
     __syncthreads();
-    if (flag[1 + WAVES]) {
+    if (flag[1 + RS_NW]) {
         if (threadIdx.x == 0) EWK_RS_ADD(9, 1);   // workgroups that drain
         rs_load_tables(a.tab64, smem);
         __syncthreads();
@@ -747,7 +791,7 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem) {
     __syncthreads();
     if (threadIdx.x == 0) {
         int any = 0;
-        for (int w = 0; w < WAVES; ++w) any |= flag[1 + w];
+        for (int w = 0; w < RS_NW; ++w) any |= flag[1 + w];
         if (any) __threadfence();
         flag[0] = __hip_atomic_fetch_add(&a.rs_ctl[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                   (int)gridDim.x - 1;
@@ -759,9 +803,9 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem) {
 #endif
     __threadfence();   // acquire what every other workgroup released before its count
     // the last workgroup: every other has drained and counted out
-    if (threadIdx.x == 0) flag[1 + WAVES] = rs_pending(ra);
+    if (threadIdx.x == 0) flag[1 + RS_NW] = rs_pending(ra);
     __syncthreads();
-    if (flag[1 + WAVES]) {
+    if (flag[1 + RS_NW]) {
         if (!loaded) {
             rs_load_tables(a.tab64, smem);
             __syncthreads();
@@ -778,7 +822,7 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem) {
 // Linear batches: the list of a k_score_f32<0> launch is drained by this launch right after
 // it (stream-ordered: the list is complete), so the batch scorer itself makes no call and keeps
 // its register allocation; every workgroup drains, the last one out resets the counters.
-__global__ __launch_bounds__(64 * WAVES, 1) void k_rescore_linear(ScoreArgs a) {
+__global__ __launch_bounds__(64 * RS_NW, 1) void k_rescore_linear(ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     score_tail<0>(a, smem);
 }
@@ -789,7 +833,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_rescore_linear(ScoreArgs a) {
 // last one drained the rest alone: 0.07 -> 0.78 ms per 8,192-stream tick); its last workgroup
 // ends the tick (counters, event watermark, poll mirror).
 template <int RING>
-__global__ __launch_bounds__(64 * WAVES, 1) void k_rescore_ring(ScoreArgs a) {
+__global__ __launch_bounds__(64 * RS_NW, 1) void k_rescore_ring(ScoreArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     score_tail<RING>(a, smem);
 }

@@ -189,6 +189,11 @@ void build_tables64(Tables64* t) {
     }
     mel_dense(t->melw_dense);
     dct_rows(t->dct);
+    // exactly (anti)symmetric rows, D[k][127 - m] = (-1)^k D[k][m]: the re-score keeps bands
+    // 0..63 of the table in LDS (ewk_rescore.h) -- the mirrored entries move by an ulp at most
+    for (int k = 0; k < NMFCC; ++k)
+        for (int m = NMEL / 2; m < NMEL; ++m)
+            t->dct[k * NMEL + m] = (k & 1) ? -t->dct[k * NMEL + NMEL - 1 - m] : t->dct[k * NMEL + NMEL - 1 - m];
     int off = 0;
     for (int m = 0; m < NMEL; ++m) {
         int lo = -1, hi = -1;

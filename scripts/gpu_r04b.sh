@@ -26,6 +26,16 @@ if [ "$MODE" = rsprobe ]; then   # per-tick re-score load and time (scripts/resc
   rc=$?; cp gpurun_out/${TAG}_cur.log gpurun_out/${TAG}_rsprobe.log; echo "rsprobe rc=$rc"; tail -50 gpurun_out/${TAG}_rsprobe.log
   exit $rc
 fi
+if [ "$MODE" = rsvar ]; then   # the re-score probe over the timing variants (scripts/build_rs_variants.py)
+  : > gpurun_out/${TAG}_rsvar.log
+  for v in ${2:-t12 t8 t12_nodct t12_nomel t12_nolog t12_nofft}; do
+    echo "== $v" >> gpurun_out/${TAG}_rsvar.log
+    EWK_LIB=$PWD/easywakeword_amd/_var/libewk_$v.so timeout -k 10 300 python -u scripts/rescore_ring_probe.py 8192 60 > gpurun_out/${TAG}_cur.log 2>&1 || exit $?
+    grep -E "^  tick|mean:|ticks with" gpurun_out/${TAG}_cur.log >> gpurun_out/${TAG}_rsvar.log
+  done
+  cat gpurun_out/${TAG}_rsvar.log
+  exit 0
+fi
 if [ "$MODE" = std ]; then   # |mean| / |std| distributions and the fp32-vs-fp64 score error by |mean|, ring path too
   timeout -k 10 600 python -u scripts/std_norm_dist.py > gpurun_out/${TAG}_cur.log 2>&1
   rc=$?; cp gpurun_out/${TAG}_cur.log gpurun_out/${TAG}_std_norm_dist.txt; echo "std rc=$rc"; tail -25 gpurun_out/${TAG}_std_norm_dist.txt
