@@ -35,6 +35,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import itertools
 import os
 import sys
 import time
@@ -173,7 +174,9 @@ def _cpu_worker(args):
     c0 = time.process_time()
     frames = 0
     n = 0
-    for x in seg_list:
+    # the worker's share of the batch, repeated until the round's time is up (single-threaded
+    # workers get through it in well under a second)
+    for x in itertools.cycle(seg_list):
         cm, cs = mfcc_ref.extract_mfcc(x.astype(np.float64))   # float64 candidate path (wakeword.py:1105-1121)
         mfcc_ref.similarity_from_stats(tm, ts, cm, cs)
         frames += 1 + len(x) // HOP
@@ -227,7 +230,7 @@ def cpu_baseline(host_pcm, lengths, offsets, seconds, rounds=3):
                      seconds / rounds, cpus[p]))
     ctx = mp.get_context("spawn")
     out_rounds = []
-    with ctx.Pool(procs, initializer=_pool_init) as pool:
+    with _OneThreadEnv(), ctx.Pool(procs, initializer=_pool_init) as pool:
         # an unreported ~1 s warm-up round first (imports, first-call and page-fault costs,
         # clock ramp: a first timed round ran 25 % below the second on one box)
         pool.map(_cpu_worker, [(j[0], 1.0, j[2]) for j in jobs], chunksize=1)
@@ -261,7 +264,8 @@ def cpu_baseline(host_pcm, lengths, offsets, seconds, rounds=3):
             "per_core": {"median": float(np.median(rates)), "min": float(rates.min()), "max": float(rates.max()),
                          "spread_pct": float(100.0 * (rates.max() - rates.min()) / np.median(rates)),
                          "unit": "frames/s per process"},
-            "sample": f"{last['segments']} segments ({last['frames']} MFCC frames) of the same ragged batch per round, "
+            "sample": f"{last['segments']} segment scorings ({last['frames']} MFCC frames; each process cycles over its "
+                      f"{per} segments of the same ragged batch) per round, "
                       f"float64 candidate path, oracle/mfcc_ref.py (numpy/scipy restatement of librosa 0.11.0 mfcc + "
                       f"scipy cosine), {procs} pinned processes x {rounds} rounds x ~{seconds / rounds:.0f} s, "
                       f"OMP_NUM_THREADS=1"}
@@ -320,7 +324,7 @@ def _cpu_stream_worker(args):
 def cpu_stream_baseline(seconds, procs):
     import multiprocessing as mp
     ctx = mp.get_context("spawn")
-    with ctx.Pool(procs, initializer=_pool_init) as pool:
+    with _OneThreadEnv(), ctx.Pool(procs, initializer=_pool_init) as pool:
         cpus = worker_cpus(procs)
         res = pool.map(_cpu_stream_worker, [(9000 + p, seconds, cpus[p]) for p in range(procs)], chunksize=1)
     rtf = sum(t * 0.1 / w for t, w in res)       # seconds of audio per second, summed over processes
@@ -335,10 +339,33 @@ def cpu_stream_baseline(seconds, procs):
                       f"oracle/mfcc_ref.py level 2 per emitted segment, OMP_NUM_THREADS=1"}
 
 
+_ONE_THREAD = {"OMP_NUM_THREADS": "1", "OPENBLAS_NUM_THREADS": "1", "MKL_NUM_THREADS": "1"}
+
+
 def _pool_init():
-    os.environ["OMP_NUM_THREADS"] = "1"
-    os.environ["OPENBLAS_NUM_THREADS"] = "1"
+    os.environ.update(_ONE_THREAD)
     sys.path.insert(0, ROOT)
+    try:   # a spawned worker imported numpy (bench.py) before this ran: cap the BLAS pool now
+        from threadpoolctl import threadpool_limits
+        threadpool_limits(1)
+    except ImportError:
+        pass
+
+
+class _OneThreadEnv:
+    """The worker pool's processes start with one BLAS / OpenMP thread each (the variables are
+    read when numpy loads, before any initializer runs): `cores` counts the threads used."""
+
+    def __enter__(self):
+        self.saved = {k: os.environ.get(k) for k in _ONE_THREAD}
+        os.environ.update(_ONE_THREAD)
+
+    def __exit__(self, *exc):
+        for k, v in self.saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 # --------------------------------------------------------------------------- streaming (config 3)
