@@ -84,19 +84,12 @@ struct RsPart {                 // one chunk: per coefficient k, rA rB sA sB sAA
     double mx;                  // log-mel max of the chunk's frames
     int32_t n;                  // frames
     int32_t flags;              // 1: a value within the ambiguity window of theta_s, 2: NaN
-    // written at listing (rs_list), so a claim reads this header and nothing else:
     int32_t slot;               // the slot this record belongs to (-1: a failed reservation)
-    int32_t seg;                // the slot's segment / event
-    int32_t len;                // its samples
-    int32_t nclaim;             // its chunks
-    int32_t base;               // its first part record
-    float theta_s;              // its speculative clamp
-    int64_t start;              // linear: offset of sample 0; ring: physical index of sample 0
-    int32_t stream;             // ring: the event's stream
-    int32_t pad[27];
+    int32_t pad[3];
 };
-// Whole 128-B lines per record: the records of one slot are written at the same time by
-// different waves, and two records sharing a line lost bytes (a few wrong fp64 scores).
+// Whole 128-B lines per record (1,152 B): the records of one slot are written at the same time
+// by different waves into uncached memory, and records sharing a line lost bytes (round 4, a
+// 1,184-B layout: a few wrong fp64 scores).
 static_assert(sizeof(RsPart) % 128 == 0, "part records own their cache lines");
 
 // Segment sources for the scorer.

@@ -1545,7 +1545,7 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, fl
             }
         }
     }
-    if (lane == 0 && near && a.rs_slots) rs_list<RING>(a, seg, len, theta_s);   // drained by the re-score launch
+    if (lane == 0 && near && a.rs_slots) rs_list(a, seg, len, theta_s);   // drained by the re-score launch
 }
 
 

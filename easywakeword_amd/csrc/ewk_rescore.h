@@ -590,7 +590,6 @@ __device__ void rs_finish(const RsArgs& a, RsSlot* sp, int seg, int T, float the
 
 // List segment `seg` (lane 0 of its scoring wave, after its float32 score is written).  Plain
 // stores: the list is read by the re-score launch that follows the scorer (stream order).
-template <int RING>
 __device__ __forceinline__ void rs_list(const ScoreArgs& a, int seg, int len, float theta_s) {
     const int s = atomicAdd(&a.rs_ctl[0], 1);
     if (s >= a.rs_cap) return;   // list full: the float32 score stands
@@ -612,55 +611,39 @@ __device__ __forceinline__ void rs_list(const ScoreArgs& a, int seg, int len, fl
     if (serial) {
         a.rs_serial[atomicAdd(&a.rs_ctl[2], 1)] = s;
         for (int c = base; c < min(base + nch, a.rs_part_cap); ++c) a.rs_parts[c].slot = -1;   // (a failed reservation)
-    } else {   // every record carries what its claim needs (one load: no slot or event reads)
-        int64_t start;
-        int32_t stream = 0;
-        if (RING) {
-            const ewk_event ev = a.events[seg];
-            start = ev.ring_start;
-            stream = ev.stream;
-        } else {
-            start = a.offsets[seg];
-        }
-        for (int c = 0; c < nch; ++c) {
-            RsPart* r = a.rs_parts + base + c;
-            r->slot = s; r->seg = seg; r->len = len; r->nclaim = nch; r->base = base; r->theta_s = theta_s;
-            r->start = start; r->stream = stream;
-        }
+    } else {
+        for (int c = 0; c < nch; ++c) a.rs_parts[base + c].slot = s;
     }
 }
 
-// Lane 0: resolve a claimed part index g (from the atomic on the part cursor) into its unit,
-// claiming again past failed reservations; once every chunk is taken, a whole serial slot.
+// Lane 0: claim the next unit -- a chunk (part record g of the reserved range, one atomic),
+// then, once every chunk is taken, a whole serial slot.
 struct RsClaim {
-    int slot = -1, unit = 0, seg = 0, T = 0, base = 0, serial = 0, nclaim = 0, len = 0, stream = 0, g = 0;
-    int64_t start = 0;
+    int slot = -1, unit = 0, seg = 0, T = 0, base = 0, serial = 0, nclaim = 0;
     float theta_s = 0.0f;
 };
-__device__ __forceinline__ int rs_take(const RsArgs& a) {
-    EWK_RS_ADD(12, 1);
-    return __hip_atomic_fetch_add(&a.rs_ctl[4], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ RsClaim rs_resolve(const RsArgs& a, int g, int n_parts, int n_serial) {
+__device__ __forceinline__ RsClaim rs_claim(const RsArgs& a, int n_parts, int n_serial) {
     RsClaim r;
-    while (g < n_parts) {
-        // the record header: {slot, seg, len, nclaim}, {base, theta_s, start}, {stream, ...}
-        const uint4* h = reinterpret_cast<const uint4*>(&a.rs_parts[g].slot);
-        const uint4 h0 = h[0], h1 = h[1], h2 = h[2];
-        if ((int)h0.x >= 0) {
-            r.slot = (int)h0.x; r.seg = (int)h0.y; r.len = (int)h0.z; r.nclaim = (int)h0.w;
-            r.base = (int)h1.x; r.theta_s = __uint_as_float(h1.y);
-            r.start = (int64_t)(((uint64_t)h1.w << 32) | h1.z); r.stream = (int)h2.x;
-            r.T = 1 + r.len / HOP; r.unit = g - r.base; r.g = g;
-            return r;
+    int s = -1;
+    for (;;) {
+        const int g = __hip_atomic_fetch_add(&a.rs_ctl[4], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        EWK_RS_ADD(12, 1);
+        if (g >= n_parts) break;
+        s = a.rs_parts[g].slot;
+        if (s >= 0) {
+            const RsSlot* p = a.rs_slots + s;
+            r.unit = g - p->base;
+            break;
         }
-        g = rs_take(a);
     }
-    const int q = __hip_atomic_fetch_add(&a.rs_ctl[5], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (q >= n_serial) return r;
-    const int s = a.rs_serial[q];
+    if (s < 0) {   // every chunk is taken: the serial slots
+        const int q = __hip_atomic_fetch_add(&a.rs_ctl[5], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (q >= n_serial) return r;
+        s = a.rs_serial[q];
+        r.unit = 0;
+    }
     const RsSlot* p = a.rs_slots + s;
-    r.slot = s; r.nclaim = p->nclaim; r.unit = 0; r.g = n_parts;
+    r.slot = s; r.nclaim = p->nclaim;
     r.seg = p->seg; r.T = p->T; r.base = p->base; r.serial = p->serial; r.theta_s = p->theta_s;
     return r;
 }
@@ -684,16 +667,9 @@ __device__ __attribute__((noinline)) bool rs_drain(const RsArgs& a, unsigned cha
     RsLane cl;
     bool have_lane = false, finished = false;
     const int n_parts = rs_n_parts(a), n_serial = rs_n_serial(a);
-    // Lane 0 claims the next chunk while this one runs (the atomic's latency behind its frames),
-    // except near the queue's end: a chunk held through a slot finish would lengthen the tail.
-    const int ahead_until = n_parts - (int)gridDim.x * RS_NW;
-    int g_next = -1;
     for (;;) {
         RsClaim c;
-        if (lane == 0) {
-            c = rs_resolve(a, g_next >= 0 ? g_next : rs_take(a), n_parts, n_serial);
-            g_next = c.slot >= 0 && !c.serial && c.g < ahead_until ? rs_take(a) : -1;
-        }
+        if (lane == 0) c = rs_claim(a, n_parts, n_serial);
         const int slot = __shfl(c.slot, 0, 64);
         if (slot < 0) break;
         const int unit = __shfl(c.unit, 0, 64), seg = __shfl(c.seg, 0, 64), T = __shfl(c.T, 0, 64);
@@ -710,17 +686,7 @@ __device__ __attribute__((noinline)) bool rs_drain(const RsArgs& a, unsigned cha
 #ifdef EWK_RS_TIMING
         const unsigned long long c0 = __builtin_amdgcn_s_memrealtime();
 #endif
-        SegView sv;   // from the record header (no event read)
-        {
-            const int len = __shfl(c.len, 0, 64), stream = __shfl(c.stream, 0, 64);
-            const int64_t start = ((int64_t)__shfl((int)(c.start >> 32), 0, 64) << 32) | (uint32_t)__shfl((int)c.start, 0, 64);
-            sv.p = RING ? (a.pcm ? a.pcm + (int64_t)stream * a.ring_len : nullptr) : a.pcm;
-            sv.p16 = RING && a.pcm16 ? a.pcm16 + (int64_t)stream * a.ring_len : nullptr;
-            sv.start = start;
-            sv.ring = RING ? a.ring_len : 0;
-            sv.len = len;
-        }
-        const RsSrc<RING> v = rs_src<RING>(sv);
+        const RsSrc<RING> v = rs_src<RING>(rs_view<RING>(a, seg));
         double pv[7], mx;
         int n, flags;
         rs_chunk(v, T, unit, (double)theta_s, kRsWindow, cl, smem, wbuf, lane, pv, mx, n, flags);
