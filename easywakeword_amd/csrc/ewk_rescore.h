@@ -596,9 +596,11 @@ __device__ __forceinline__ void rs_list(const ScoreArgs& a, int seg, int len, fl
     const int T = 1 + len / HOP;
     const int nch = (T + kRsFrames - 1) / kRsFrames;
     int serial = a.list_all, base = 0;   // list_all (every segment): one wave each, no part records
+    bool failed = false;
     if (!serial) {
         base = atomicAdd(&a.rs_ctl[1], nch);
-        if (base > a.rs_part_cap - nch) serial = 1;   // part pool full: this slot runs serially
+        failed = base < 0 || base > a.rs_part_cap - nch;   // part pool full (or the cursor wrapped)
+        if (failed) serial = 1;                             // this slot runs serially
     }
     RsSlot* p = a.rs_slots + s;
     p->seg = seg;
@@ -610,7 +612,8 @@ __device__ __forceinline__ void rs_list(const ScoreArgs& a, int seg, int len, fl
     p->serial = serial;
     if (serial) {
         a.rs_serial[atomicAdd(&a.rs_ctl[2], 1)] = s;
-        for (int c = base; c < min(base + nch, a.rs_part_cap); ++c) a.rs_parts[c].slot = -1;   // (a failed reservation)
+        if (failed && base >= 0)   // the reserved records inside the pool: nobody's chunks
+            for (int c = base; c < min(base + nch, a.rs_part_cap); ++c) a.rs_parts[c].slot = -1;
     } else {
         for (int c = 0; c < nch; ++c) a.rs_parts[base + c].slot = s;
     }
@@ -703,7 +706,13 @@ __device__ __attribute__((noinline)) bool rs_drain(const RsArgs& a, unsigned cha
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int last = 0;
         if (lane == 0) last = __hip_atomic_fetch_add(&sp->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nclaim - 1;
-        if (__shfl(last, 0, 64)) {   // (the part loads below issue after the count returned)
+        if (__shfl(last, 0, 64)) {
+            // Acquire (agent scope, lowered to buffer_inv sc1): the other waves' part records are
+            // read through this CU's vector L1, which may still hold lines of the same records
+            // from an earlier tick; the invalidate drops them.  The writers' side needs no
+            // release: records are uncached memory (stores complete at memory, s_waitcnt
+            // vmcnt(0) above orders them before the count).
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
 #ifdef EWK_RS_TIMING
             const unsigned long long f0 = __builtin_amdgcn_s_memrealtime();
 #endif
