@@ -14,30 +14,41 @@
 //             [t*160-256, t*160+256) of the segment, zero outside; T = 1+L//160.
 //             Samples come through a buffer descriptor whose range check returns 0
 //             outside the segment (the padding); ring segments wrap at the stream ring.
-//   pass    : 16 frames per wave = one log-mel tile, four lanes per frame (ewk_fp4.h):
-//             the tile's 2,912 samples staged in LDS by LDS-DMA one pass ahead, an in-register
-//             FFT whose cross-lane steps are v_permlane16/32_swap row exchanges, the untangle
-//             in-lane, mel partial sums reduced over the frame's four lanes, log.
+//   staging : a wave pass is 8 frames spanning 1,632 contiguous samples, loaded one
+//             pass ahead with coalesced dword loads and stored to LDS with
+//             ds_write_addtid_b32.
+//   FFT     : 16 lanes per frame, two frames per 16-lane group (8 frames per pass: two
+//             independent instruction streams per lane).  The 512-point real frame is
+//             packed as 256 complex points z[n] = x[2n] + i x[2n+1]; 256 = 16 x 16
+//             four-step FFT: a register DFT16 (window folded into its first stage,
+//             tan-factored W16 twiddles), a twiddle, an LDS transpose, a second DFT16,
+//             then the real-FFT untangle with each bin and its conjugate partner in the
+//             same lane (no cross-lane traffic).
+//   mel     : Slaney bands from LDS, fully unrolled with compile-time group widths
+//             (band m = j + 16 i; widths {2,2,2,3,4,6,9,12}, weights zero-padded), then
+//             10*log10(max(1e-10, .)) via v_log_f32; written to a 16-frame log-mel tile
+//             as f16 hi/lo pairs (hi = x truncated to 11 bits, lo = x - hi).
 //   DCT     : the only dense GEMM on the path: C[32 x 16] = D[32 x 128] . X[128 x 16]
-//             per tile on the matrix cores, v_mfma_f32_16x16x32_f16 on f16 hi/lo splits
-//             (Dh Xh + Dh Xl + Dl Xh, f32 accumulation), operands B straight from the pass's
-//             registers, rows 20..31 zero.
+//             per 16-frame tile on the matrix cores, v_mfma_f32_16x16x32_f16 on the hi/lo
+//             splits (Dh Xh + Dh Xl + Dl Xh, f32 accumulation), rows 20..31 zero.
 //   top_db  : power_to_db clamps at (segment max - 80 dB), a segment-global coupling.
-//             Tiles are processed loudest first (a scout) and each is clamped at the
-//             running max - 80 dB (exact once the max is known); at the end only the tiles
-//             whose stored minimum is below the final max - 80 dB are recomputed and their
-//             contribution swapped in the statistics (nothing is written to global memory
-//             but the results).
+//             Pass 1 clamps each tile speculatively at the running max - 80 dB (exact
+//             once the max is known) and records the stored tile minimum; if the segment
+//             min is below the final max - 80 dB, pass 2 recomputes only the tiles whose
+//             stored minimum is below it and swaps their contribution in the statistics
+//             (nothing is written to global memory but the results).
 //   stats   : population mean/std over frames from fp64 shifted sums
 //             (d = c - c[frame 0]) -- exact 0 std for identical frames.
 //   score   : the reference's own float32 / float64 cosine arithmetic
 //             (wakeword.py:611-625 + scipy correlation); NaN kept.  Near-threshold
-//             scores are re-scored by the fp64 path (ewk_rescore.h).
+//             scores are re-scored by k_score_f64 (fp64 path, below).
 #include <hip/hip_runtime.h>
 #include <math.h>
 
-#include "ewk_fp4.h"
 #include "ewk_internal.h"
+
+// s_setprio 1 over the frame-pass LDS phases (window, transposes, mel): -0.4 %
+#define EWK_SETPRIO(v) __builtin_amdgcn_s_setprio(v)
 
 // Per-wave phase timing of the linear-batch scorer (debug builds with -DEWK_TIMING only:
 // scripts/mb_score.py prints it; the product build compiles none of it).  dbg[k] sums the
@@ -47,11 +58,16 @@
 #define EWK_DBG_ARG , dbg
 #define EWK_TS(v) const uint64_t v = __builtin_amdgcn_s_memtime()
 #define EWK_TADD(k, a, b) dbg[k] += (b) - (a)
+// frame-pass sub-phases (dbg[12..18]) and passes timed (dbg[19]); tile_passes passes nullptr
+#define EWK_PASS_PARAM , uint64_t* pdbg
+#define EWK_PASS_ARG(x) , x
 #else
 #define EWK_DBG_PARAM
 #define EWK_DBG_ARG
 #define EWK_TS(v)
 #define EWK_TADD(k, a, b)
+#define EWK_PASS_PARAM
+#define EWK_PASS_ARG(x)
 #endif
 #ifdef EWK_TIMING
 constexpr int kDbgN = 20;
@@ -65,34 +81,264 @@ __device__ unsigned long long g_ewk_dbg[kDbgN];
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
-// LDS carve (bytes, every offset a multiple of 16): the pass tables (ewk_fp4.h), then per
-// wave: the staged samples of one pass (filled by LDS-DMA), a 480-B scratch for the
-// statistics (finish_stats, the cooperative ring mode's sums) and the top_db records.
-constexpr int kFPP = fp4::FPP;                             // frames per pass = per tile
-constexpr int L_TAB = 0;
-constexpr int L_WAVES = fp4::TABLE_BYTES;
-constexpr int W_STAGE = 0;
-constexpr int W_PD = W_STAGE + fp4::STAGE_BYTES;            // 20 x 3 doubles
-// per-tile record of the speculative top_db clamp (segment_stats): the stored log-mel minimum,
-// the clamp and the processing order (3 x kSpecTiles ints)
-constexpr int kSpecTiles = 64;   // tiles of frames 0..1023 (10.2 s) are recorded and scout-ordered
-constexpr int W_SPEC = W_PD + 480;
-constexpr int kSpecRun = kSpecTiles;                       // spec[kSpecRun + tile]: the tile's clamp
-constexpr int kSpecOrder = kSpecRun + kSpecTiles;          // spec[kSpecOrder + k]: k-th tile processed
+// LDS carve (bytes, every offset a multiple of 16).  The per-lane table rows are
+// transposed to [lane j][index] with a 144-B (36-dword) row pitch so one
+// ds_read_b128 fetches 2 float2 entries and a 16-lane group spans all 64 banks.
+// Frames per wave pass: kNF per 16-lane group (kNF = 2: two independent FFTs per lane).
+constexpr int kFPP = 4 * kNF;
+constexpr int kStageLoads = ((kFPP - 1) * HOP + NFFT + 63) / 64;   // dword loads per lane per pass
+// frame fr's FFT scratch starts at scr_frame_off(fr) (ewk_internal.h)
+constexpr int kScrFrames = kFPP * SCR_FRAME + 8 * (kNF - 1);
+// kNF = 2: a lane's two frames are consecutive (slot (g, f) = frame 2f + g of the pass),
+// so the second frame's first 11 sample pairs are the first frame's pairs 5..15 (hop 160 =
+// 5 x 32) and only 5 more are read.  The stage is skewed -- sample s at s + 32 floor(s / 320)
+// -- so the four lane groups' frames (320 samples apart) land 32 banks apart.
+__host__ __device__ constexpr int stg_off(int c) { return 256 * c + 128 * (c / 5); }   // bytes of stage row c
+__host__ __device__ constexpr int win_off(int g, int n1) {   // bytes: pair n1 of slot g from the lane's base
+    return 4 * (160 * g + 32 * n1 + 32 * ((160 * g + 32 * n1) / 320));
+}
+constexpr int kStageFloats = stg_off(kStageLoads) / 4;
+constexpr int kScrFloats = (kScrFrames > kStageFloats) ? kScrFrames : kStageFloats;
+// The per-wave FFT scratch (also the sample staging) comes first in LDS: the M0 base of
+// ds_write_addtid_b32 is 16 bits wide, so every wave's scratch must start below 64 KB.
+constexpr int SCR_BYTES = (kScrFloats * 4 + 15) & ~15;
+constexpr int L_SCR = 0;                                  // [wave] kFPP frames x 272 floats
+constexpr int L_TAB = L_SCR + WAVES * SCR_BYTES;
+static_assert(L_SCR + (WAVES - 1) * SCR_BYTES < 65536, "ds_write_addtid_b32 bases must fit M0[15:0]");
+
+// LDS carve (bytes, every offset a multiple of 16).  The per-lane table rows are
+// transposed to [lane j][index] with a 144-B (36-dword) row pitch so one
+// ds_read_b128 fetches 2 float2 entries and a 16-lane group spans all 64 banks.
+constexpr int TP = 18;                                    // float2 pitch of a [j][16] table row
+constexpr int WP = 52;                                    // float pitch of the [j][48] mel weight row (13 chunks: b128/b64 conflict free)
+constexpr int L_WIN2 = L_TAB;                             // [j][n1] = win2[16*n1 + j]
+constexpr int L_TW1 = L_WIN2 + 16 * TP * 8;               // [j][k1-1] = tw1[16*k1 + j], k1 = 1..15
+constexpr int L_TW2 = L_TW1 + 16 * TP * 8;                // [j][k2] = tw2[j + 16*k2]
+constexpr int L_WPAD = L_TW2 + 16 * TP * 8;               // [j][kMelOff[i] + q] = wpad[16*(it0_i + q) + j]
+constexpr int L_BLO = L_WPAD + 16 * WP * 4;
+constexpr int L_DCT = L_BLO + NMEL * 4;
+// DCT operand image for v_mfma_f32_16x16x32_f16: D * 2^10 split into f16 hi + lo (the
+// products hi*hi + hi*lo + lo*hi carry ~22 bits).  The tile's k order groups each lane's
+// eight bands: k-chunk c (k = 8c .. 8c+7) holds bands c + 16 jj, jj = 0..7, so the
+// operand of k-step q for lane l is chunk 4q + (l >> 4).  Row tile 0 (coefficients 0..15):
+// [q][hi/lo][lane] 16-B chunks; row tile 1 (coefficients 16..19): [q][hi/lo][l >> 4][l & 3]
+// for the lanes with (l & 15) < 4, every other lane reads the block's zero chunk.
+constexpr float kDctScale = 1024.0f;
+constexpr float kTopDbUnits = 80.0f;   // top_db, in the tile's dB units
+constexpr int DCT_RT1 = 4 * 2 * 64 * 16;                  // row tile 1: [q][hi/lo] blocks of 17 chunks
+constexpr int DCT_RT1_STRIDE = 17 * 16;                   // 16 data chunks [l >> 4][l & 3] + a zero chunk
+constexpr int DCT_BYTES = DCT_RT1 + 8 * DCT_RT1_STRIDE;
+constexpr int L_SHARED_END = ((L_DCT + DCT_BYTES) + 15) & ~15;
+constexpr int W_TILE = 0;                                 // 16 frame rows x 512 B of f16 hi/lo chunks (tile_chunk)
+// per-tile record of the speculative top_db clamp (segment_stats): stored log-mel minima per
+// pass, the clamps and the processing order ((passes per tile + 2) x kSpecTiles ints)
+constexpr int kSpecTiles = 48;   // tiles of frames 0..767 (7.7 s) are recorded and scout-ordered
+constexpr int W_SPEC = W_TILE + 16 * NMEL * 4;
+constexpr int kSpecRun = (16 / kFPP) * kSpecTiles;      // spec[kSpecRun + tile]: the tile's clamp
+constexpr int kSpecOrder = kSpecRun + kSpecTiles;        // spec[kSpecOrder + k]: k-th tile processed
 constexpr int W_BYTES = W_SPEC + (kSpecOrder + kSpecTiles) * 4;
-constexpr int L_WG = L_WAVES + WAVES * W_BYTES;            // ring mode: segment index + per-wave log-mel max/min
+constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
 constexpr int LDS_BYTES = L_WG + 16 + 8 * WAVES;
 constexpr int kRescoreFrames = 16;
 constexpr double kTinyMean = 64.0;  // |mean vector| below which the fp64 path decides
                                     // (loud audio, c0 cancelling: DESIGN.md numerics)
 constexpr double kTinyStd = 20.0;   // |std vector| below which the fp64 path decides (bench batch >= 24.8,
                                     // streaming events >= 32.5: scripts/std_norm_dist.py)
-constexpr float kTopDbUnits = 80.0f;   // top_db, in the tile's dB units
 static_assert(LDS_BYTES <= 160 * 1024, "the workgroup must fit a CU's LDS");
-static_assert(W_BYTES % 16 == 0 && fp4::TABLE_BYTES % 16 == 0, "LDS carve alignment");
-static_assert(kSpecTiles <= 64, "the scout ranks one tile per lane");
+static_assert(16 % kFPP == 0, "passes must tile the 16-frame log-mel tile");
+
 
 __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
+// Eight ds_read_b128 of consecutive 16-B chunks issued together, and their wait.
+// Written as asm so the scheduler cannot sink each read next to its first use (at
+// 256 VGPRs it does, and every read then costs a full LDS round trip).
+#define EWK_LD128(r, a, c) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(r[c]) : "v"(a), "i"(16 * (c)) : "memory")
+#define EWK_LD128_8(r, addr)                                                                        \
+    do {                                                                                           \
+        const uint32_t _a = (addr);                                                                \
+        EWK_LD128(r, _a, 0); EWK_LD128(r, _a, 1); EWK_LD128(r, _a, 2); EWK_LD128(r, _a, 3);         \
+        EWK_LD128(r, _a, 4); EWK_LD128(r, _a, 5); EWK_LD128(r, _a, 6); EWK_LD128(r, _a, 7);         \
+    } while (0)
+#define EWK_WAIT_8(r)                                                                              \
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(r[0]), "+v"(r[1]), "+v"(r[2]), "+v"(r[3]), "+v"(r[4]), \
+                 "+v"(r[5]), "+v"(r[6]), "+v"(r[7]) : : "memory")
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 w) {
+    return make_float2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
+}
+
+__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
+    const float2 t0 = make_float2(a0.x + a2.x, a0.y + a2.y);
+    const float2 t1 = make_float2(a0.x - a2.x, a0.y - a2.y);
+    const float2 t2 = make_float2(a1.x + a3.x, a1.y + a3.y);
+    const float2 t3 = make_float2(a1.x - a3.x, a1.y - a3.y);
+    a0 = make_float2(t0.x + t2.x, t0.y + t2.y);
+    a2 = make_float2(t0.x - t2.x, t0.y - t2.y);
+    a1 = make_float2(t1.x + t3.y, t1.y - t3.x);   // t1 - i t3
+    a3 = make_float2(t1.x - t3.y, t1.y + t3.x);   // t1 + i t3
+}
+
+// Second radix-4 stage of the DFT16 with its W16 twiddles folded into FMAs.  Each
+// twiddle is written as a real scale times a (1, tan) factor -- W^1 = C1 (1 - iT),
+// W^3 = C1 (T - i), W^9 = C1 (-1 + iT), W^2 = R2 (1 - i), W^6 = R2 (-1 - i), T = tan(pi/8)
+// -- the two twiddled inputs of a butterfly pair share the scale, and the scale rides
+// in the FMAs of the butterfly outputs: 22 / 20 / 22 instructions for rows k1 = 1 / 2 / 3
+// instead of 28 / 24 / 28 (three complex multiplies + a radix-4 butterfly).
+__device__ __forceinline__ void dft16_stage2(float2 (&x)[16]) {
+    constexpr float C1 = 0.92387953251128674f, R2 = 0.70710678118654752f, T = 0.41421356237309505f;
+    dft4(x[0], x[1], x[2], x[3]);
+    {   // k1 = 1: twiddles W^1, W^2, W^3
+        const float2 a0 = x[4], y1 = x[5], y2 = x[6], y3 = x[7];
+        const float2 u2 = make_float2(y2.x + y2.y, y2.y - y2.x);                        // Y2 (1 - i)
+        const float2 t0 = make_float2(fmaf(R2, u2.x, a0.x), fmaf(R2, u2.y, a0.y));
+        const float2 t1 = make_float2(fmaf(-R2, u2.x, a0.x), fmaf(-R2, u2.y, a0.y));
+        const float2 u1 = make_float2(fmaf(T, y1.y, y1.x), fmaf(-T, y1.x, y1.y));       // Y1 (1 - iT)
+        const float2 u3 = make_float2(fmaf(T, y3.x, y3.y), fmaf(T, y3.y, -y3.x));       // Y3 (T - i)
+        const float2 v2 = make_float2(u1.x + u3.x, u1.y + u3.y), v3 = make_float2(u1.x - u3.x, u1.y - u3.y);
+        x[4] = make_float2(fmaf(C1, v2.x, t0.x), fmaf(C1, v2.y, t0.y));
+        x[6] = make_float2(fmaf(-C1, v2.x, t0.x), fmaf(-C1, v2.y, t0.y));
+        x[5] = make_float2(fmaf(C1, v3.y, t1.x), fmaf(-C1, v3.x, t1.y));                // t1 - i C1 v3
+        x[7] = make_float2(fmaf(-C1, v3.y, t1.x), fmaf(C1, v3.x, t1.y));                // t1 + i C1 v3
+    }
+    {   // k1 = 2: twiddles W^2, W^4 = -i, W^6
+        const float2 a0 = x[8], y1 = x[9], y2 = x[10], y3 = x[11];
+        const float2 t0 = make_float2(a0.x + y2.y, a0.y - y2.x);                        // a0 + (-i Y2)
+        const float2 t1 = make_float2(a0.x - y2.y, a0.y + y2.x);
+        const float2 u1 = make_float2(y1.x + y1.y, y1.y - y1.x);                        // Y1 (1 - i)
+        const float d3 = y3.y - y3.x, n3 = y3.x + y3.y;                                 // Y3 (-1 - i) = (d3, -n3)
+        const float2 v2 = make_float2(u1.x + d3, u1.y - n3), v3 = make_float2(u1.x - d3, u1.y + n3);
+        x[8] = make_float2(fmaf(R2, v2.x, t0.x), fmaf(R2, v2.y, t0.y));
+        x[10] = make_float2(fmaf(-R2, v2.x, t0.x), fmaf(-R2, v2.y, t0.y));
+        x[9] = make_float2(fmaf(R2, v3.y, t1.x), fmaf(-R2, v3.x, t1.y));
+        x[11] = make_float2(fmaf(-R2, v3.y, t1.x), fmaf(R2, v3.x, t1.y));
+    }
+    {   // k1 = 3: twiddles W^3, W^6, W^9
+        const float2 a0 = x[12], y1 = x[13], y2 = x[14], y3 = x[15];
+        const float d2 = y2.y - y2.x, n2 = y2.x + y2.y;                                 // Y2 (-1 - i) = (d2, -n2)
+        const float2 t0 = make_float2(fmaf(R2, d2, a0.x), fmaf(-R2, n2, a0.y));
+        const float2 t1 = make_float2(fmaf(-R2, d2, a0.x), fmaf(R2, n2, a0.y));
+        const float2 u1 = make_float2(fmaf(T, y1.x, y1.y), fmaf(T, y1.y, -y1.x));       // Y1 (T - i)
+        const float m3 = fmaf(T, y3.y, y3.x), u3y = fmaf(T, y3.x, -y3.y);               // Y3 (-1 + iT) = (-m3, u3y)
+        const float2 v2 = make_float2(u1.x - m3, u1.y + u3y), v3 = make_float2(u1.x + m3, u1.y - u3y);
+        x[12] = make_float2(fmaf(C1, v2.x, t0.x), fmaf(C1, v2.y, t0.y));
+        x[14] = make_float2(fmaf(-C1, v2.x, t0.x), fmaf(-C1, v2.y, t0.y));
+        x[13] = make_float2(fmaf(C1, v3.y, t1.x), fmaf(-C1, v3.x, t1.y));
+        x[15] = make_float2(fmaf(-C1, v3.y, t1.x), fmaf(C1, v3.x, t1.y));
+    }
+}
+
+// In-place radix-4x4 DFT16.  On return x[4*k1 + k2] holds X[k1 + 4*k2].
+__device__ __forceinline__ void dft16_perm(float2 (&x)[16]) {
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) dft4(x[n2], x[4 + n2], x[8 + n2], x[12 + n2]);
+    dft16_stage2(x);
+}
+
+// dft16_perm of the windowed input (x[n].x w[n].x, x[n].y w[n].y): the window products
+// ride in the first stage's FMAs (t0 = fma(x0, w0, x2 w2), t1 = fma(x0, w0, -x2 w2)).
+__device__ __forceinline__ void dft16_perm_win(float2 (&x)[16], const float2 (&w)[16]) {
+#pragma unroll
+    for (int n2 = 0; n2 < 4; ++n2) {
+        const float2 x0 = x[n2], x1 = x[4 + n2], x2 = x[8 + n2], x3 = x[12 + n2];
+        const float2 w0 = w[n2], w1 = w[4 + n2], w2 = w[8 + n2], w3 = w[12 + n2];
+        const float2 p2 = make_float2(x2.x * w2.x, x2.y * w2.y), p3 = make_float2(x3.x * w3.x, x3.y * w3.y);
+        const float2 t0 = make_float2(fmaf(x0.x, w0.x, p2.x), fmaf(x0.y, w0.y, p2.y));
+        const float2 t1 = make_float2(fmaf(x0.x, w0.x, -p2.x), fmaf(x0.y, w0.y, -p2.y));
+        const float2 t2 = make_float2(fmaf(x1.x, w1.x, p3.x), fmaf(x1.y, w1.y, p3.y));
+        const float2 t3 = make_float2(fmaf(x1.x, w1.x, -p3.x), fmaf(x1.y, w1.y, -p3.y));
+        x[n2] = make_float2(t0.x + t2.x, t0.y + t2.y);
+        x[8 + n2] = make_float2(t0.x - t2.x, t0.y - t2.y);
+        x[4 + n2] = make_float2(t1.x + t3.y, t1.y - t3.x);   // t1 - i t3
+        x[12 + n2] = make_float2(t1.x - t3.y, t1.y + t3.x);  // t1 + i t3
+    }
+    dft16_stage2(x);
+}
+
+// Natural-order accessor of dft16_perm's output: X[k] lives in slot perm(k).
+__device__ __forceinline__ constexpr int dperm(int k) { return 4 * (k & 3) + (k >> 2); }
+
+
+// f16 hi/lo split of a float32: hi = x truncated to f16's 11 significant bits (exact in
+// f16 over the dB range), lo = x - hi exactly, stored to f16 with round-to-nearest, so
+// float(hi) + float(lo) = x within 2^-22 |x|.
+__device__ __forceinline__ float f16_trunc(float x) { return __uint_as_float(__float_as_uint(x) & 0xFFFFE000u); }
+typedef _Float16 halfx2 __attribute__((ext_vector_type(2)));
+typedef _Float16 halfx8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ uint32_t pk_f16(float a, float b) {   // v_cvt_pk_f16_f32
+    halfx2 h;
+    h.x = (_Float16)a;
+    h.y = (_Float16)b;
+    return __builtin_bit_cast(uint32_t, h);
+}
+__device__ __forceinline__ float f16_lo(uint32_t p) { return (float)__builtin_bit_cast(halfx2, p).x; }
+__device__ __forceinline__ float f16_hi(uint32_t p) { return (float)__builtin_bit_cast(halfx2, p).y; }
+// eight log-mel values -> their hi chunk and lo chunk (16 B each)
+// hi pair = v_cvt_pkrtz_f16_f32 (round toward zero = the 11-bit truncation over the dB
+// range), lo = f16(x - float(hi)) by v_fma_mixlo/mixhi_f16 (the subtraction in f32, exact;
+// one rounding to f16): 3 VALU per pair instead of 6.
+__device__ __forceinline__ void split2(float a, float b, uint32_t& h, uint32_t& l) {
+    h = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b));
+    uint32_t r;
+    asm("v_fma_mixlo_f16 %0, %1, 1.0, -%2 op_sel_hi:[0,0,1]\n\t"
+        "v_fma_mixhi_f16 %0, %3, 1.0, -%2 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+        : "=&v"(r) : "v"(a), "v"(h), "v"(b));
+    l = r;
+}
+__device__ __forceinline__ void split8(const float (&x)[8], uint4& hi, uint4& lo) {
+    split2(x[0], x[1], hi.x, lo.x);
+    split2(x[2], x[3], hi.y, lo.y);
+    split2(x[4], x[5], hi.z, lo.z);
+    split2(x[6], x[7], hi.w, lo.w);
+}
+// Byte offset of k-chunk c of frame row r in the log-mel tile: the row's hi chunks fill its
+// first 256 B and the lo chunks the next 256 B, chunk c at slot c ^ r, so the 16 rows of a
+// DCT operand read (one chunk per row) and the 16 chunks of a row write both cover all
+// 64 banks.
+__device__ __forceinline__ int tile_chunk(int r, int c) { return 512 * r + 16 * (c ^ r); }
+
+// top_db clamp of a log-mel tile (its flat 8 KB LDS image): lane l takes the chunk pairs
+// p = l + 64 u (frame row p >> 4, slot p & 15), rebuilds each value exactly as
+// float(hi) + float(lo), clamps it at theta and writes the re-split pair back in place.
+__device__ __forceinline__ void clamp_load(const float4* src, int lane, uint4 (&h)[4], uint4 (&l)[4]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int p = lane + 64 * u;
+        h[u] = __builtin_bit_cast(uint4, src[32 * (p >> 4) + (p & 15)]);
+        l[u] = __builtin_bit_cast(uint4, src[32 * (p >> 4) + 16 + (p & 15)]);
+    }
+}
+__device__ __forceinline__ void clamp_store(float* tile, int lane, const uint4 (&h)[4], const uint4 (&l)[4],
+                                            float theta) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const uint32_t hw[4] = {h[u].x, h[u].y, h[u].z, h[u].w}, lw[4] = {l[u].x, l[u].y, l[u].z, l[u].w};
+        float x[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            x[2 * k] = fmaxf(f16_lo(hw[k]) + f16_lo(lw[k]), theta);
+            x[2 * k + 1] = fmaxf(f16_hi(hw[k]) + f16_hi(lw[k]), theta);
+        }
+        uint4 hh, ll;
+        split8(x, hh, ll);
+        const int p = lane + 64 * u;
+        uint4* dst = reinterpret_cast<uint4*>(tile) + 32 * (p >> 4) + (p & 15);
+        dst[0] = hh;
+        dst[16] = ll;
+    }
+}
+
+// FFT transpose image of one pass (one real or imaginary plane): row k1 of frame set g
+// holds the 64 lanes' values (16 f + j) contiguously, as ds_write_addtid_b32 stores them
+// (address = M0 + offset + 4 lane).  Rows are placed so that the untangle's row reads
+// -- lane (f, h, j') fetches rows j' and 16 - j' (8 for j' = 0) of frame set h with
+// ds_read_b128 -- hit 16 distinct bank quads in every lane group: the row of (r, h)
+// starts at quad (j'(r) & 3) + 8 h (mod 16), rows sorted by that shift.
+__host__ __device__ constexpr int tr_off(int r, int h) {
+    const int jp = r < 8 ? r : (r == 8 ? 0 : 16 - r);
+    const int q = (jp >> 2) + (r >= 8 ? 2 : 0);
+    return 64 * (16 * h + 4 * (jp & 3) + q) + 4 * ((jp & 3) + 8 * h);   // floats
+}
 
 // Segment samples through a buffer descriptor: the hardware range check returns 0
 // outside [0, len) (negative offsets wrap to huge unsigned ones), which is exactly
@@ -128,19 +374,462 @@ __device__ __forceinline__ SegSrc<RING> make_src(const void* p, int64_t start, i
     return v;
 }
 
-// Stage tile `tile` (frames 16 tile .. 16 tile + 15, samples 2,560 tile - 256 ..) into the
-// wave's span: LDS-DMA for float32 sources (no VGPRs, lands while the current pass computes),
-// registers for int16 rings.
+// Coalesced staging loads: lane l fetches samples q0 + 64*c + l, c < kStageLoads.
 template <int RING>
-__device__ __forceinline__ void stage_tile(const SegSrc<RING>& v, int tile, float* stage, int lane) {
-    const int S0 = tile * kFPP * HOP - NFFT / 2;
-    if (RING == 0) fp4::stage_dma_linear(v.rsrc, S0, stage, lane);
-    else if (RING == 1) fp4::stage_dma_ring(v.rsrc, S0, v.len, v.wrap_at, v.start, stage, lane);
-    else fp4::stage_i16_ring(v.rsrc, S0, v.len, v.wrap_at, v.start, stage, lane);
+__device__ __forceinline__ void stage_load(const SegSrc<RING>& v, int q0, int lane, float (&r)[kStageLoads]) {
+#pragma unroll
+    for (int c = 0; c < kStageLoads; ++c) {
+        const int q = q0 + 64 * c + lane;
+        int off;
+        if (RING) {
+            const int phys = q >= v.wrap_at ? q - v.wrap_at : q + v.start;
+            off = (unsigned)q < (unsigned)v.len ? phys * sample_bytes(RING) : -1;
+        } else {
+            off = q * 4;
+        }
+        if (RING == 2)   // buffer_load_sshort + v_cvt_f32_i32: the int16 sample, exactly
+            r[c] = (float)(short)__builtin_amdgcn_raw_buffer_load_b16(v.rsrc, off, 0, 0);
+        else
+            r[c] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(v.rsrc, off, 0, 0));
+    }
 }
-// the staged samples have landed (LDS-DMA counts in vmcnt; the int16 path's stores are
-// ordered before the pass's reads by the wave's in-order LDS queue)
-__device__ __forceinline__ void stage_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// 13 lane-contiguous rows of 64 floats with ds_write_addtid_b32 (M0 = stage base, saved
+// and restored; s_nop 0 for the M0 -> LDS hazard): half the LDS cycles of ds_write_b32
+#define EWK_ST13(o)                                                                                            \
+    asm volatile("s_mov_b32 %[sv], m0\n\ts_mov_b32 m0, %[base]\n\ts_nop 0\n\t"                              \
+                 "ds_write_addtid_b32 %[r0] offset:%[o0]\n\tds_write_addtid_b32 %[r1] offset:%[o1]\n\t"          \
+                 "ds_write_addtid_b32 %[r2] offset:%[o2]\n\tds_write_addtid_b32 %[r3] offset:%[o3]\n\t"          \
+                 "ds_write_addtid_b32 %[r4] offset:%[o4]\n\tds_write_addtid_b32 %[r5] offset:%[o5]\n\t"          \
+                 "ds_write_addtid_b32 %[r6] offset:%[o6]\n\tds_write_addtid_b32 %[r7] offset:%[o7]\n\t"          \
+                 "ds_write_addtid_b32 %[r8] offset:%[o8]\n\tds_write_addtid_b32 %[r9] offset:%[o9]\n\t"          \
+                 "ds_write_addtid_b32 %[r10] offset:%[o10]\n\tds_write_addtid_b32 %[r11] offset:%[o11]\n\t"      \
+                 "ds_write_addtid_b32 %[r12] offset:%[o12]\n\ts_mov_b32 m0, %[sv]"                                 \
+                 : [sv] "=&s"(m0save)                                                                          \
+                 : [base] "s"(m0base), [r0] "v"(r[o]), [r1] "v"(r[o + 1]), [r2] "v"(r[o + 2]), [r3] "v"(r[o + 3]), \
+                   [r4] "v"(r[o + 4]), [r5] "v"(r[o + 5]), [r6] "v"(r[o + 6]), [r7] "v"(r[o + 7]),                \
+                   [r8] "v"(r[o + 8]), [r9] "v"(r[o + 9]), [r10] "v"(r[o + 10]), [r11] "v"(r[o + 11]),          \
+                   [r12] "v"(r[o + 12]), [o0] "i"(stg_off(o)), [o1] "i"(stg_off(o + 1)), [o2] "i"(stg_off(o + 2)), \
+                   [o3] "i"(stg_off(o + 3)), [o4] "i"(stg_off(o + 4)), [o5] "i"(stg_off(o + 5)),                    \
+                   [o6] "i"(stg_off(o + 6)), [o7] "i"(stg_off(o + 7)), [o8] "i"(stg_off(o + 8)),                    \
+                   [o9] "i"(stg_off(o + 9)), [o10] "i"(stg_off(o + 10)), [o11] "i"(stg_off(o + 11)),                \
+                   [o12] "i"(stg_off(o + 12))                                                                     \
+                 : "memory")
+static_assert(kStageLoads == 26, "stage_store writes two blocks of 13 rows");
+__device__ __forceinline__ void stage_store(float* stage, int lane, const float (&r)[kStageLoads]) {
+    const uint32_t m0base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)stage);
+    uint32_t m0save;
+    EWK_ST13(0);
+    EWK_ST13(13);
+}
+
+constexpr int kMelW[8] = {2, 2, 2, 3, 4, 6, 9, 12};   // per 16-band group (checked on the host)
+constexpr int kMelIt0[8] = {0, 2, 4, 6, 9, 13, 19, 28};    // first weight of group i in Tables::wpad
+// Each group's weights start on a b64 (widths 2) or b128 boundary of the LDS row so one
+// group is fetched with 1-3 wide reads right before it is used.
+constexpr int kMelOff[8] = {0, 2, 4, 8, 12, 16, 24, 36};
+constexpr int kMelRow = 48;
+static_assert(kMelRow <= WP && WP % 4 == 0, "mel weight rows");
+
+// Column writes of one frame set's transpose image (one plane: real or imaginary), with
+// ds_write_addtid_b32 (address = M0 + offset + 4 lane).
+template <int G>
+__device__ __forceinline__ void xpose_write(const float2 (&ag)[16], int half, uint32_t m0base) {
+    constexpr int g = G;
+    float w[16];
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1) w[k1] = half ? ag[dperm(k1)].y : ag[dperm(k1)].x;
+    // M0 is compiler-reserved: saved and restored in the same statement; the
+    // s_nop covers the M0-write -> LDS-use hazard (without it the stores use the old M0)
+    uint32_t m0save;
+    asm volatile("s_mov_b32 %[sv], m0\n\ts_mov_b32 m0, %[base]\n\ts_nop 0\n\t"
+                 "ds_write_addtid_b32 %[w0] offset:%[o0]\n\tds_write_addtid_b32 %[w1] offset:%[o1]\n\t"
+                 "ds_write_addtid_b32 %[w2] offset:%[o2]\n\tds_write_addtid_b32 %[w3] offset:%[o3]\n\t"
+                 "ds_write_addtid_b32 %[w4] offset:%[o4]\n\tds_write_addtid_b32 %[w5] offset:%[o5]\n\t"
+                 "ds_write_addtid_b32 %[w6] offset:%[o6]\n\tds_write_addtid_b32 %[w7] offset:%[o7]\n\t"
+                 "ds_write_addtid_b32 %[w8] offset:%[o8]\n\tds_write_addtid_b32 %[w9] offset:%[o9]\n\t"
+                 "ds_write_addtid_b32 %[w10] offset:%[o10]\n\tds_write_addtid_b32 %[w11] offset:%[o11]\n\t"
+                 "ds_write_addtid_b32 %[w12] offset:%[o12]\n\tds_write_addtid_b32 %[w13] offset:%[o13]\n\t"
+                 "ds_write_addtid_b32 %[w14] offset:%[o14]\n\tds_write_addtid_b32 %[w15] offset:%[o15]\n\t"
+                 "s_mov_b32 m0, %[sv]"
+                 : [sv] "=&s"(m0save)
+                 : [base] "s"(m0base), [w0] "v"(w[0]), [w1] "v"(w[1]), [w2] "v"(w[2]), [w3] "v"(w[3]),
+                   [w4] "v"(w[4]), [w5] "v"(w[5]), [w6] "v"(w[6]), [w7] "v"(w[7]), [w8] "v"(w[8]),
+                   [w9] "v"(w[9]), [w10] "v"(w[10]), [w11] "v"(w[11]), [w12] "v"(w[12]),
+                   [w13] "v"(w[13]), [w14] "v"(w[14]), [w15] "v"(w[15]),
+                   [o0] "i"(4 * tr_off(0, g)), [o1] "i"(4 * tr_off(1, g)), [o2] "i"(4 * tr_off(2, g)),
+                   [o3] "i"(4 * tr_off(3, g)), [o4] "i"(4 * tr_off(4, g)), [o5] "i"(4 * tr_off(5, g)),
+                   [o6] "i"(4 * tr_off(6, g)), [o7] "i"(4 * tr_off(7, g)), [o8] "i"(4 * tr_off(8, g)),
+                   [o9] "i"(4 * tr_off(9, g)), [o10] "i"(4 * tr_off(10, g)), [o11] "i"(4 * tr_off(11, g)),
+                   [o12] "i"(4 * tr_off(12, g)), [o13] "i"(4 * tr_off(13, g)), [o14] "i"(4 * tr_off(14, g)),
+                   [o15] "i"(4 * tr_off(15, g))
+                 : "memory");
+}
+
+// One kFPP-frame pass: frames t0 .. t0 + kFPP - 1, samples already staged in `scr`.
+// Writes rows [row0, row0 + kFPP) of the log-mel tile (clamped at clampv) and returns the
+// per-lane max/min of the valid (unclamped) log-mel values.  If next_t0 >= 0, the samples
+// of the pass starting at frame next_t0 are fetched meanwhile and staged at the end.
+// `lo[i]` = first bin of band j + 16 i (per lane, loaded once per kernel).
+template <int RING>
+__device__ __forceinline__ void frame_pass(const SegSrc<RING>& v, int t0, int T, int row0, int next_t0,
+                                           const unsigned char* smem, float* scr, float* tile,
+                                           int lane, const int (&lo)[8], float& vmax, float& vmin, float& nanp,
+                                           float clampv EWK_PASS_PARAM) {
+    EWK_TS(fp0);
+    EWK_SETPRIO(1);
+    // lane group f = lane>>4 holds frames fr = 4 g + f (g < kNF) of this pass; the
+    // kNF frames of a lane are independent instruction streams (ILP for the wave).
+    const int f = lane >> 4, j = lane & 15;
+    // after the transpose lane (h, j') = (j >> 3, j & 7) owns bin columns rowA = j' and
+    // rowB = 16 - j' (8 for j' = 0) of frame 4h + f (scratch scf)
+    const int jp = j & 7;
+    const int rowA = jp, rowB = jp ? 16 - jp : 8;
+    float* scf = scr + scr_frame_off(4 * (j >> 3) + f);
+    bool valid[kNF];
+    float* sc[kNF];
+#pragma unroll
+    for (int g = 0; g < kNF; ++g) {
+        valid[g] = t0 + 2 * f + g < T;
+        sc[g] = scr + scr_frame_off(4 * g + f);
+    }
+
+    // ---- window the staged samples: lane j holds z[16*n1 + j] = x[32*n1+2j] + i x[32*n1+2j+1]
+    // (single ds_read_b64s: the compiler would pair them into ds_read2_b64, which
+    // costs the LDS twice the cycles per byte)
+    float2 a[kNF][16];
+    floatx4 t4[8];   // twiddle row W256^(j*k1)
+    {
+        float2 x[kNF][16];
+        {
+            const uint32_t sa = (uint32_t)(uintptr_t)(scr + 352 * f + 2 * j);
+#define EWK_LD64(g, n) asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(x[g][n]) : "v"(sa), "i"(win_off(g, n)) : "memory")
+            EWK_LD64(0, 0); EWK_LD64(0, 1); EWK_LD64(0, 2); EWK_LD64(0, 3); EWK_LD64(0, 4); EWK_LD64(0, 5);
+            EWK_LD64(0, 6); EWK_LD64(0, 7); EWK_LD64(0, 8); EWK_LD64(0, 9); EWK_LD64(0, 10); EWK_LD64(0, 11);
+            EWK_LD64(0, 12); EWK_LD64(0, 13); EWK_LD64(0, 14); EWK_LD64(0, 15);
+            EWK_LD64(1, 11); EWK_LD64(1, 12); EWK_LD64(1, 13); EWK_LD64(1, 14); EWK_LD64(1, 15);
+#undef EWK_LD64
+        }
+        floatx4 w4[8];   // this lane's window pairs, fetched in the same batch
+        EWK_LD128_8(w4, (uint32_t)(uintptr_t)(reinterpret_cast<const float4*>(smem + L_WIN2) + j * (TP / 2)));
+        EWK_WAIT_8(w4);
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(x[0][0]), "+v"(x[0][1]), "+v"(x[0][2]), "+v"(x[0][3]), "+v"(x[0][4]), "+v"(x[0][5]),
+                       "+v"(x[0][6]), "+v"(x[0][7]), "+v"(x[0][8]), "+v"(x[0][9]), "+v"(x[0][10]), "+v"(x[0][11]),
+                       "+v"(x[0][12]), "+v"(x[0][13]), "+v"(x[0][14]), "+v"(x[0][15])
+                     :
+                     : "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(x[1][11]), "+v"(x[1][12]), "+v"(x[1][13]), "+v"(x[1][14]), "+v"(x[1][15])
+                     :
+                     : "memory");
+#pragma unroll
+        for (int n = 0; n <= 10; ++n) x[1][n] = x[0][n + 5];   // the shared sample pairs
+        float2 wv[16];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            wv[2 * c] = make_float2(w4[c].x, w4[c].y);
+            wv[2 * c + 1] = make_float2(w4[c].z, w4[c].w);
+        }
+        EWK_SETPRIO(0);
+        // ---- DFT16 over n1 (window folded into its first stage), twiddle W256^(j*k1)
+        // (one twiddle row serves every frame of the lane, requested before the DFT16s)
+        EWK_LD128_8(t4, (uint32_t)(uintptr_t)(reinterpret_cast<const float4*>(smem + L_TW1) + j * (TP / 2)));
+#pragma unroll
+        for (int g = 0; g < kNF; ++g) {
+#pragma unroll
+            for (int n = 0; n < 16; ++n) a[g][n] = x[g][n];
+            dft16_perm_win(a[g], wv);
+        }
+    }
+    lds_order();
+    EWK_TS(fp1);
+    // next pass's samples: issued before the mel stage (registers are free there),
+    // stored to the staging area at the end of the pass
+    float pf[kStageLoads];
+    {
+        EWK_WAIT_8(t4);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const floatx4 w = t4[c];   // k1 = 2c+1, 2c+2
+#pragma unroll
+            for (int g = 0; g < kNF; ++g) {
+                a[g][dperm(2 * c + 1)] = cmul(a[g][dperm(2 * c + 1)], make_float2(w.x, w.y));
+                if (c < 7) a[g][dperm(2 * c + 2)] = cmul(a[g][dperm(2 * c + 2)], make_float2(w.z, w.w));
+            }
+        }
+    }
+    EWK_TS(fp2);
+    EWK_SETPRIO(1);
+    // ---- transpose through LDS (real, then imaginary half): lane k1 <- A_{n2}[k1].
+    // Row r (16 floats) keeps column n in 4-float chunk (n>>2) ^ ((r>>2)&3): the
+    // column writes (ds_write_b32, the frames of a 32-lane half 272 floats apart) and
+    // the row reads (ds_read_b128) are both bank-conflict free.
+    float2 b[kNF][16];
+    {
+        const uint32_t m0base = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)scr);
+        const int offA = tr_off(rowA, j >> 3) + 16 * f, offB = tr_off(rowB, j >> 3) + 16 * f;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+#pragma unroll
+            for (int g = 0; g < kNF; ++g) {
+                if (g == 0) xpose_write<0>(a[0], half, m0base);
+                else xpose_write<1>(a[1], half, m0base);
+            }
+            lds_order();
+            // lane (h, j') = (j >> 3, j & 7) reads two columns of frame 4h + f: c0 = j' and its
+            // conjugate partner 16 - j' (column 8 beside column 0 for j' = 0)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const float4* rd = reinterpret_cast<const float4*>(scr + (s2 ? offB : offA));
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const float4 q = rd[c];
+                    if (half) {
+                        b[s2][4 * c].y = q.x; b[s2][4 * c + 1].y = q.y; b[s2][4 * c + 2].y = q.z; b[s2][4 * c + 3].y = q.w;
+                    } else {
+                        b[s2][4 * c].x = q.x; b[s2][4 * c + 1].x = q.y; b[s2][4 * c + 2].x = q.z; b[s2][4 * c + 3].x = q.w;
+                    }
+                }
+            }
+            lds_order();
+        }
+    }
+    EWK_TS(fp3);
+    EWK_SETPRIO(0);
+    // ---- DFT16 over n2: Z[j + 16*k2] = b[dperm(k2)]
+#pragma unroll
+    for (int g = 0; g < kNF; ++g) dft16_perm(b[g]);
+    EWK_TS(fp4);
+    // ---- untangle + power, two conjugate bins per step, no cross-lane traffic.  For
+    // k = c0 + 16 it the partner Zp = Z[256 - k] sits in this lane's other column; with
+    // A = Z[k] + conj(Zp), B = Z[k] - conj(Zp), C = i W512^k B:
+    //   P'[k] = |2 X[k]|^2 = |A - C|^2,  P'[256 - k] = |A + C|^2.
+    // Lanes j' = 1..7: it = 0..15 (it = 16 repeats it = 15).  Lane j' = 0 pairs column
+    // 0 with itself (it = 0..8: k = 16 it, 256 - k; it = 0 yields bin 256) and column 8
+    // with itself (it = 9..16: k = 8 + 16 (it - 9)).
+    {
+        const bool z0 = jp == 0;
+        // the 17 twiddles of this lane class, fetched up front (9 ds_read_b128): read one
+        // step ahead they cost an LDS round trip per step behind that step's writes
+        float2 tw[18];
+        {
+            const float4* t4 = reinterpret_cast<const float4*>(smem + L_TW2) + jp * (TP / 2);   // [j'][it], 17 entries
+#pragma unroll
+            for (int c = 0; c < 9; ++c) {
+                const float4 q = t4[c];
+                tw[2 * c] = make_float2(q.x, q.y);
+                tw[2 * c + 1] = make_float2(q.z, q.w);
+            }
+        }
+        float* pA0 = scf + rowA;                     // P[k]      at pA0[16 it]       (it <= 15)
+        float* pA1 = z0 ? scf - 136 : pA0;           //           lane 0, it >= 9
+        float* pA2 = z0 ? scf - 136 : pA0 - 16;      //           it = 16
+        float* pB0 = scf - rowA;                     // P[256-k]  at pB0[256 - 16 it]
+        float* pB1 = z0 ? scf + 136 : pB0;
+        float* pB2 = z0 ? scf + 136 : pB0 + 16;
+        // two steps per iteration, their stores grouped by base (pa, pa, pb, pb) so that
+        // the stores of consecutive steps merge into ds_write2_b32
+#pragma unroll
+        for (int it0 = 0; it0 < 17; it0 += 2) {
+            float py[2], px[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int it = it0 + u;
+                if (it >= 17) break;
+                const float2 w = tw[it];   // (cos, tan)(2 pi k / 512)
+                const float2 ug = b[0][dperm(it < 16 ? it : 15)];
+                const float2 vg = b[1][dperm(it < 16 ? 15 - it : 0)];
+                float2 uu, vv;
+                if (it <= 8) {
+                    uu = ug;
+                    const float2 vz = b[0][dperm((16 - it) & 15)];
+                    vv = z0 ? vz : vg;
+                } else {
+                    const float2 uz = b[1][dperm(it - 9)], vz = b[1][dperm(24 - it)];
+                    uu = z0 ? uz : ug;
+                    vv = z0 ? vz : vg;
+                }
+                const float ar = uu.x + vv.x, ai = uu.y - vv.y;
+                const float br = uu.x - vv.x, bi = uu.y + vv.y;
+                // w = (c, t = s / c): C = c (t br - bi, t bi + br), its scale in the output FMAs
+                const float er = fmaf(w.y, br, -bi), ei = fmaf(w.y, bi, br);
+                const float yr = fmaf(-w.x, er, ar), yi = fmaf(-w.x, ei, ai);
+                const float xr = fmaf(w.x, er, ar), xi = fmaf(w.x, ei, ai);
+                py[u] = yr * yr + yi * yi;
+                px[u] = xr * xr + xi * xi;
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int it = it0 + u;
+                if (it >= 17) break;
+                float* pa = it <= 8 ? pA0 : (it < 16 ? pA1 : pA2);
+                pa[16 * it] = py[u];
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int it = it0 + u;
+                if (it >= 17) break;
+                float* pb = it <= 8 ? pB0 : (it < 16 ? pB1 : pB2);
+                pb[256 - 16 * it] = px[u];
+            }
+        }
+        // the zero pad (bins 257..271) the unrolled band loops read past bin 256
+        scf[257 + jp] = 0.0f;
+        if (jp < 7) scf[265 + jp] = 0.0f;
+    }
+    lds_order();
+    EWK_TS(fp5);
+    EWK_SETPRIO(1);
+    if (next_t0 >= 0) stage_load(v, next_t0 * HOP - NFFT / 2, lane, pf);
+    // ---- mel + log: lane j computes bands m = j + 16*i of its frames (weights shared).
+    // The stage's LDS reads go in two batches (band groups 0-5, then 6-7: 19 and 21
+    // weights), each followed by its FMAs -- one wait per batch, not one per group.
+    float db[kNF][8];
+    {
+        const float* wrow = reinterpret_cast<const float*>(smem + L_WPAD) + j * WP;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+            const int i0 = hh ? 6 : 0, i1 = hh ? 8 : 6;
+            float wv[MEL_ITERS], pv[kNF][MEL_ITERS];
+#pragma unroll
+            for (int i = i0; i < i1; ++i) {
+                if (kMelW[i] <= 2) {
+                    const float2 w = *reinterpret_cast<const float2*>(wrow + kMelOff[i]);
+                    wv[kMelIt0[i]] = w.x; wv[kMelIt0[i] + 1] = w.y;
+                } else {
+#pragma unroll
+                    for (int c = 0; c < (kMelW[i] + 3) / 4; ++c) {
+                        const float4 w = *reinterpret_cast<const float4*>(wrow + kMelOff[i] + 4 * c);
+                        const float ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (4 * c + e < kMelW[i]) wv[kMelIt0[i] + 4 * c + e] = ww[e];
+                    }
+                }
+#pragma unroll
+                for (int g = 0; g < kNF; ++g) {
+                    const float* sp = sc[g] + lo[i];
+#pragma unroll
+                    for (int q = 0; q < kMelW[i]; ++q) pv[g][kMelIt0[i] + q] = sp[q];
+                }
+            }
+#pragma unroll
+            for (int i = i0; i < i1; ++i)
+#pragma unroll
+                for (int g = 0; g < kNF; ++g) {
+                    float acc = 0.0f;
+#pragma unroll
+                    for (int q = 0; q < kMelW[i]; ++q) acc = fmaf(wv[kMelIt0[i] + q], pv[g][kMelIt0[i] + q], acc);
+                    // 10*log10(x) = (10*log10(2)) * log2(x), v_log_f32
+                    db[g][i] = 3.0102999566398120f * __log2f(fmaxf(1e-10f, acc));
+                    // NaN probe: a NaN sample makes every bin of its frame NaN, which the
+                    // amin floor above would hide (fmax returns the number); the reference's
+                    // np.maximum propagates it and scores NaN (acc * 0 is NaN for NaN / Inf)
+                    if (i == 0) nanp = fmaf(acc, 0.0f, nanp);
+                }
+        }
+    }
+    EWK_SETPRIO(0);
+    lds_order();
+    EWK_TS(fp6);
+    // Rows of frames past T keep their (finite: silence gives -100 dB) values: the DCT
+    // columns are independent and the statistics skip those frames, so only the frame's
+    // max/min needs the validity test, once per frame.  The eight bands of a lane form
+    // k-chunk j of its frame row (hi and lo halves, one ds_write_b128 each).
+#pragma unroll
+    for (int g = 0; g < kNF; ++g) {
+        const int r = row0 + 2 * f + g;
+        float fmx = db[g][0], fmn = db[g][0], x[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            fmx = fmaxf(fmx, db[g][i]);
+            fmn = fminf(fmn, db[g][i]);
+            x[i] = fmaxf(db[g][i], clampv);   // top_db recompute path; -inf folds away otherwise
+        }
+        vmax = fmaxf(vmax, valid[g] ? fmx : -INFINITY);
+        vmin = fminf(vmin, valid[g] ? fmn : INFINITY);
+        uint4 hi, lo;
+        split8(x, hi, lo);
+        unsigned char* tb = reinterpret_cast<unsigned char*>(tile) + tile_chunk(r, j);
+        *reinterpret_cast<uint4*>(tb) = hi;
+        *reinterpret_cast<uint4*>(tb + 256) = lo;
+    }
+    lds_order();
+    if (next_t0 >= 0) stage_store(scr, lane, pf);
+    lds_order();
+#ifdef EWK_TIMING
+    EWK_TS(fp7);
+    if (pdbg) {
+        pdbg[12] += fp1 - fp0; pdbg[13] += fp2 - fp1; pdbg[14] += fp3 - fp2; pdbg[15] += fp4 - fp3;
+        pdbg[16] += fp5 - fp4; pdbg[17] += fp6 - fp5; pdbg[18] += fp7 - fp6; pdbg[19] += 1;
+    }
+#endif
+}
+
+// DCT of one 16-frame log-mel tile on the matrix cores: C[32 x 16] = D[32 x 128] X[128 x 16]
+// with v_mfma_f32_16x16x32_f16 on the f16 hi/lo splits, three products per k-step
+// (Dh Xh + Dh Xl + Dl Xh, f32 accumulation; the dropped Dl Xl is ~2^-22 relative).
+// Lane l gets C[row = 4h + r][frame col] of both row tiles (h = l>>4, col = l&15) in
+// c[0..3], c[4..7] -- the layout of the f32 16x16x4 MFMA.  The operands of k-step q
+// (6 ds_read_b128) are requested one step ahead of its 6 MFMAs.
+#define EWK_DCT_RD(dst, addr, off) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(off) : "memory")
+#define EWK_DCT_LOAD(p, q)                                                   \
+    do {                                                                     \
+        EWK_DCT_RD(Bh[p], bq[q], 0);                                         \
+        EWK_DCT_RD(Bl[p], bq[q], 256);                                       \
+        EWK_DCT_RD(A0h[p], a0, 2048 * (q));                                  \
+        EWK_DCT_RD(A0l[p], a0, 2048 * (q) + 1024);                           \
+        EWK_DCT_RD(A1h[p], a1, DCT_RT1_STRIDE * (2 * (q)));                  \
+        EWK_DCT_RD(A1l[p], a1, DCT_RT1_STRIDE * (2 * (q) + 1));              \
+    } while (0)
+#define EWK_DCT_WAIT(p, n)                                                                               \
+    asm volatile("s_waitcnt lgkmcnt(" #n ")"                                                             \
+                 : "+v"(Bh[p]), "+v"(Bl[p]), "+v"(A0h[p]), "+v"(A0l[p]), "+v"(A1h[p]), "+v"(A1l[p]) \
+                 :                                                                                       \
+                 : "memory")
+#define EWK_MF(a, b, acc) \
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(halfx8, a), __builtin_bit_cast(halfx8, b), acc, 0, 0, 0)
+#define EWK_DCT_MFMA(p)                                                                        \
+    do {                                                                                       \
+        EWK_MF(A0h[p], Bh[p], acc0); EWK_MF(A1h[p], Bh[p], acc1);                              \
+        EWK_MF(A0h[p], Bl[p], acc0); EWK_MF(A1h[p], Bl[p], acc1);                              \
+        EWK_MF(A0l[p], Bh[p], acc0); EWK_MF(A1l[p], Bh[p], acc1);                              \
+    } while (0)
+__device__ __forceinline__ void tile_dct(const float* tile, const float* s_dct, int lane, float (&c)[8]) {
+    const int col = lane & 15, g4 = lane >> 4;
+    floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+    // B of k-step q: chunk 4q + g4 of frame row col, at slot (4q + g4) ^ col =
+    // 4 (q ^ (col >> 2)) + (g4 ^ (col & 3))
+    const uint32_t tb = (uint32_t)(uintptr_t)tile + 512 * col + 16 * (g4 ^ (col & 3));
+    uint32_t bq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bq[q] = tb + 64 * (q ^ (col >> 2));
+    const uint32_t db = (uint32_t)(uintptr_t)s_dct;
+    const uint32_t a0 = db + 16 * lane;
+    const uint32_t a1 = db + DCT_RT1 + 16 * (col < 4 ? 4 * g4 + col : 16);
+    floatx4 Bh[2], Bl[2], A0h[2], A0l[2], A1h[2], A1l[2];
+    EWK_DCT_LOAD(0, 0);
+    EWK_DCT_LOAD(1, 1);
+    EWK_DCT_WAIT(0, 6);
+    EWK_DCT_MFMA(0);
+    EWK_DCT_LOAD(0, 2);
+    EWK_DCT_WAIT(1, 6);
+    EWK_DCT_MFMA(1);
+    EWK_DCT_LOAD(1, 3);
+    EWK_DCT_WAIT(0, 6);
+    EWK_DCT_MFMA(0);
+    EWK_DCT_WAIT(1, 0);
+    EWK_DCT_MFMA(1);
+    lds_order();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { c[i] = acc0[i] * (1.0f / kDctScale); c[4 + i] = acc1[i] * (1.0f / kDctScale); }
+}
+#undef EWK_DCT_RD
+#undef EWK_DCT_LOAD
+#undef EWK_DCT_WAIT
+#undef EWK_DCT_MFMA
+#undef EWK_MF
 
 // fp64 shifted sums of the frame columns that exist (d = c - cref).
 __device__ __forceinline__ void stats_add(const float (&c)[8], const float (&cref)[8], bool ok, double (&s1)[8],
@@ -258,6 +947,81 @@ __device__ __forceinline__ void finish_stats(int T, const float (&cref)[8], doub
     }
     lds_order();
 }
+
+// Zero the kFPP tile rows of one pass (frames past T).
+__device__ __forceinline__ void zero_rows(float* tile, int row0, int lane) {
+    for (int m = lane; m < kFPP * NMEL; m += 64) tile[row0 * NMEL + m] = 0.0f;
+}
+
+// The tiles of one segment that pass 1 left holding a value below the final max - 80 dB
+// are recomputed: the stored tile (clamped at its speculative `run`, rebuilt bit for bit
+// by the same frame passes) gives the pass-1 DCT columns to remove, the tile clamped at
+// theta in LDS the columns to add.  (Parking every tile in global memory for this pass
+// instead wrote 10 KB per 16 frames -- 2.3x the algorithmic traffic -- for the ~16 % of
+// bench tiles that need it; recomputing those costs the same time.  Parking only the tiles
+// the scout ranks within 3 dB of a later one -- 2.8 per bench segment, 0.47 of them fixed --
+// lost 1.5 % too: the parking stores hold up the next pass's vmcnt waits, and a reload
+// costs 2/3 of a recompute.  profiles/r03_v2_park_ab.txt.  Rebuilding a self-clamped tile's
+// stored image exactly -- its clamp at the run before it, then at its own -- so that the
+// columns taken out equal the ones put in to the last bit cost 1.3 %, for score changes of
+// ~1e-9: the fix-up recomputes at the tile's final run.  A full-coverage scout (Hann-weighted
+// frame energies from every sample, scripts/scout_sim.py H8) cut the recomputes from 0.53 to
+// 0.11 tiles per bench segment but its loads cost 4x the time saved: r03_v3_scout_ab.txt.)
+// Passes of one tile; `mask` bit p selects pass p (the others' rows are zeroed, like the
+// rows of frames past T).
+constexpr int kPassesPerTile = 16 / kFPP;
+constexpr int kAllPasses = (1 << kPassesPerTile) - 1;
+template <int RING>
+__device__ __forceinline__ void tile_passes(const SegSrc<RING>& v, int tile_i, int T, const unsigned char* smem,
+                                            float* scr, float* tile, int lane, const int (&lo)[8], float& mx,
+                                            float& mn, float& nanp, float clampv, int mask = kAllPasses) {
+    const int npass = (T + kFPP - 1) / kFPP;
+    const int p0 = tile_i * kPassesPerTile;
+    mask &= npass - p0 >= kPassesPerTile ? kAllPasses : (1 << max(0, npass - p0)) - 1;
+    if (mask) {   // stage the tile's first selected pass
+        float r[kStageLoads];
+        stage_load(v, (p0 + __builtin_ctz(mask)) * kFPP * HOP - NFFT / 2, lane, r);
+        stage_store(scr, lane, r);
+        lds_order();
+    }
+#pragma unroll 1
+    for (int p = 0; p < kPassesPerTile; ++p) {
+        if ((mask >> p) & 1) {
+            const int rest = mask >> (p + 1);   // the next selected pass of this tile is prefetched
+            frame_pass(v, (p0 + p) * kFPP, T, p * kFPP, rest ? (p0 + p + 1 + __builtin_ctz(rest)) * kFPP : -1,
+                       smem, scr, tile, lane, lo, mx, mn, nanp, clampv EWK_PASS_ARG(nullptr));
+        } else {   // frames past T, or a pass left out: zero rows (their columns are not used)
+            zero_rows(tile, p * kFPP, lane);
+        }
+    }
+    lds_order();
+}
+
+// The passes in `mask` of a tile whose stored values (clamped at `run`) include some below
+// the final threshold: recomputed bit for bit, their DCT columns swapped from clamped-at-run
+// to clamped-at-theta in the shifted sums.  A pass whose stored minimum is >= theta is
+// unchanged and skipped (per-pass records, segment_stats).
+template <int RING>
+__device__ __forceinline__ void fix_tile(const SegSrc<RING>& v, int tile_i, int T, float run, float theta,
+                                         const unsigned char* smem, float* scr, float* tile, int lane,
+                                         const int (&lo)[8], const float (&cref)[8], double (&s1)[8],
+                                         double (&s2)[8], int mask = kAllPasses) {
+    const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
+    float d0 = 0.f, d1 = 0.f, d2 = 0.f;
+    tile_passes(v, tile_i, T, smem, scr, tile, lane, lo, d0, d1, d2, run, mask);
+    float co[8], cn[8];
+    tile_dct(tile, s_dct, lane, co);
+    {
+        uint4 h[4], l[4];
+        clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
+        clamp_store(tile, lane, h, l, theta);
+    }
+    lds_order();
+    tile_dct(tile, s_dct, lane, cn);
+    const int col = lane & 15;
+    stats_replace(cn, co, cref, tile_i * 16 + col < T && ((mask >> (col / kFPP)) & 1), s1, s2);
+}
+
 // Scout of a segment's tiles (tile t: frames 16t .. 16t + 15): the energy of 4 x 64 of its
 // samples (one 64-sample row every 640), wave-reduced; lane t returns the estimate for tile
 // t (t < ntile <= 64).  Only a processing-order heuristic: the results do not depend on it.
@@ -361,43 +1125,25 @@ __device__ __forceinline__ void work_describe(const WorkCtx& c, WorkAhead& w) {
     }
 }
 
-// The tile of one segment that pass 1 left holding a value below the final max - 80 dB is
-// recomputed (the same pass, bit-identical values): the DCT of its values clamped at its
-// speculative `run` gives the pass-1 columns to remove, clamped at theta the columns to add.
-// (Rounds 1-4 measured the alternatives: parking every tile in global memory, parking only
-// the tiles the scout ranks close to a later one, exact fix-ups of self-clamped tiles, a
-// full-coverage scout -- each cost more than the recomputes it saved)
-template <int RING>
-__device__ __forceinline__ void fix_tile(const SegSrc<RING>& v, int tile_i, int T, float run, float theta,
-                                         const unsigned char* tabs, float* stage, int lane, const float (&cref)[8],
-                                         double (&s1)[8], double (&s2)[8]) {
-    stage_tile(v, tile_i, stage, lane);
-    stage_wait();
-    float lm[32], d0 = -INFINITY, d1 = INFINITY, d2 = 0.0f;
-    fp4::pass(tabs, stage, lane, true, lm, d0, d1, d2, [] {});
-    float co[8], cn[8];
-    fp4::dct(lm, run, tabs, lane, co);
-    fp4::dct(lm, theta, tabs, lane, cn);
-    stats_replace(cn, co, cref, tile_i * kFPP + (lane & 15) < T, s1, s2);
-}
-
 // Whole segment for one wave.  spec: this wave's per-tile record in LDS -- the stored
-// log-mel minimum of tile i in spec[i], its speculative clamp in spec[kSpecRun + i] (tiles
-// past kSpecTiles are stored unclamped and always recomputed when theta bites), then the
-// processing order (spec[kSpecOrder + k]).
+// log-mel minimum of pass p of tile i in spec[kPassesPerTile * i + p], the tile's
+// speculative clamp in spec[kSpecRun + i] (tiles past kSpecTiles are stored unclamped and
+// always recomputed when theta bites), then the processing order (spec[kSpecOrder + k]).
 //
 // The top_db clamp (max - 80 dB over the whole segment) is applied speculatively at the
 // running max, which each tile updates before its DCT; a tile that already holds the
 // segment max needs no fix, so the tiles are processed loudest first by a scout estimate
-// (bench batch: 16 % of the tiles recomputed in time order, ~5 % in scout order).  Each
-// tile's samples are staged by LDS-DMA while the previous tile computes.
+// (bench batch: 16 % of the tiles recomputed in time order, ~5 % in scout order), and only
+// the passes of a tile that hold a value below the final threshold are recomputed.
 template <int RING>
-__device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* tabs, float* stage, float* spec, double* pd,
-                              int lane, double (&s1)[8], double (&s2)[8], float& theta_out, const WorkCtx& wc,
-                              WorkAhead& nx EWK_DBG_PARAM) {
+__device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, float* scr, float* tile,
+                              float* spec, int lane, const int (&lo)[8], double (&s1)[8], double (&s2)[8],
+                              float& theta_out, const WorkCtx& wc, WorkAhead& nx EWK_DBG_PARAM) {
     EWK_TS(tq0);
+    const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     const int T = 1 + v.len / HOP;
-    const int ntile = (T + kFPP - 1) / kFPP;
+    const int ntile = (T + 15) >> 4;
+    const int npass = (T + kFPP - 1) / kFPP;
     const int col = lane & 15;
     int* order = reinterpret_cast<int*>(spec + kSpecOrder);
     const bool ordered = ntile > 1 && ntile <= kSpecTiles;
@@ -419,43 +1165,64 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* tabs, 
     for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
     float vmax = -INFINITY, vmin = INFINITY, nanp = 0.0f;
     int tile_i = ordered ? order[0] : 0;
-    stage_tile(v, tile_i, stage, lane);
+    {   // stage the first pass synchronously
+        float r[kStageLoads];
+        stage_load(v, tile_i * 16 * HOP - NFFT / 2, lane, r);
+        stage_store(scr, lane, r);
+        lds_order();
+    }
+    EWK_TS(tq2);
+    EWK_TADD(2, tq1, tq2);
     float run = -INFINITY;   // speculative clamp: running max - 80 dB
     for (int k = 0; k < ntile; ++k) {
         EWK_TS(tk0);
         const int next_tile = k + 1 < ntile ? (ordered ? order[k + 1] : k + 1) : -1;
         const bool rec = tile_i < kSpecTiles;
+        float tmw = INFINITY;
         if (!rec) run = -INFINITY;
         const bool last = k + 1 == ntile;
         if (last && wc.ahead) work_claim<RING>(wc, nx, lane);
-        stage_wait();
-        float lm[32], tp = INFINITY;
-#ifdef EWK_FP4_SYNC   // debug: synchronous staging, no prefetch
-        fp4::pass(tabs, stage, lane, tile_i * kFPP + col < T, lm, vmax, tp, nanp, [] {});
-        if (next_tile >= 0) stage_tile(v, next_tile, stage, lane);
-#else
-        fp4::pass(tabs, stage, lane, tile_i * kFPP + col < T, lm, vmax, tp, nanp, [&] {
-            if (next_tile >= 0) stage_tile(v, next_tile, stage, lane);
-        });
-#endif
-        const float tmw = wave_min(tp);   // this tile's minimum (its record below)
+#pragma unroll 1
+        for (int p = 0; p < kPassesPerTile; ++p) {
+            const int pass = tile_i * kPassesPerTile + p;
+            // the next pass to prefetch: this tile's next, else the next tile's first
+            const int nxt = p + 1 < kPassesPerTile && pass + 1 < npass ? (pass + 1) * kFPP
+                                                                      : (next_tile >= 0 ? next_tile * 16 : -1);
+            float tp = INFINITY;
+            if (pass < npass)
+                frame_pass(v, pass * kFPP, T, p * kFPP, nxt, smem, scr, tile, lane, lo, vmax, tp, nanp, run EWK_PASS_ARG(dbg));
+            else   // rows of frames past T: zero (ignored by the statistics)
+                zero_rows(tile, p * kFPP, lane);
+            const float tpw = wave_min(tp);   // this pass's minimum (its record below)
+            tmw = fminf(tmw, tpw);
+            if (lane == 0 && rec) spec[kPassesPerTile * tile_i + p] = tpw;
+        }
+        lds_order();
         EWK_TS(tk1);
         EWK_TADD(3, tk0, tk1);
         if (last && wc.ahead) work_order<RING>(wc, nx);
         // max(max(x, run), final) = max(x, final): a tile stored clamped at the running max
         // (this tile's own values included) is exact unless a later tile raises the max
         const float run2 = rec ? wave_max(vmax) - kTopDbUnits : -INFINITY;
+        if (run2 > run && tmw < run2) {   // this tile raised the max over some of its own values
+            uint4 h[4], l[4];
+            clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
+            clamp_store(tile, lane, h, l, run2);
+            lds_order();
+        }
         run = fmaxf(run, run2);
         float c[8];
-        fp4::dct(lm, run, tabs, lane, c);
+        tile_dct(tile, s_dct, lane, c);
         if (k == 0) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
         }
-        stats_add(c, cref, tile_i * kFPP + col < T, s1, s2);
+        stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
         vmin = fminf(vmin, tmw);
-        if (lane == 0 && rec) {   // stored minimum: the tile's minimum as clamped at its run
-            spec[tile_i] = fmaxf(tmw, run);
+        if (lane == 0 && rec) {   // stored minima: the pass minima as clamped at the tile's run
+#pragma unroll
+            for (int p = 0; p < kPassesPerTile; ++p)
+                spec[kPassesPerTile * tile_i + p] = fmaxf(spec[kPassesPerTile * tile_i + p], run);
             spec[kSpecRun + tile_i] = run;
         }
         tile_i = next_tile;
@@ -472,11 +1239,19 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* tabs, 
         lds_order();
         for (int cur = 0; cur < ntile; ++cur) {
             const bool rec = cur < kSpecTiles;
-            if (rec && !(spec[cur] < theta)) continue;   // no stored value below theta
+            int mask = kAllPasses;
+            if (rec) {   // only the passes holding a stored value below theta change
+                mask = 0;
+#pragma unroll
+                for (int p = 0; p < kPassesPerTile; ++p) mask |= (spec[kPassesPerTile * cur + p] < theta ? 1 : 0) << p;
+                if (!mask) continue;
+            }
 #ifdef EWK_TIMING
             dbg[10] += 1;
+            dbg[11] += __builtin_popcount(mask);
 #endif
-            fix_tile(v, cur, T, rec ? spec[kSpecRun + cur] : -INFINITY, theta, tabs, stage, lane, cref, s1, s2);
+            fix_tile(v, cur, T, rec ? spec[kSpecRun + cur] : -INFINITY, theta, smem, scr, tile, lane, lo, cref, s1,
+                     s2, mask);
         }
     }
     if (__ballot(nanp != nanp)) {   // NaN input: NaN statistics, NaN score (like the reference)
@@ -485,7 +1260,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* tabs, 
     }
     EWK_TS(tq4);
     EWK_TADD(5, tq3, tq4);
-    finish_stats(T, cref, s1, s2, lane, pd);
+    finish_stats(T, cref, s1, s2, lane, reinterpret_cast<double*>(scr));
     EWK_TS(tq5);
     EWK_TADD(6, tq4, tq5);
 }
@@ -498,12 +1273,13 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* tabs, 
 //   S1 = sum_w s1_w + n_w d_w,  S2 = sum_w s2_w + 2 d_w s1_w + n_w d_w^2,  d_w = cref_w - cref_0.
 // Leaves mean / std (fp32-rounded) in misc0[0..19], misc0[20..39] (wave 0's scratch).
 template <int RING>
-__device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, float* stage, float* spec, double* pd,
-                                   int wave, int lane, float* misc0, float& theta_out) {
-    const unsigned char* tabs = smem + L_TAB;
+__device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, float* scr, float* tile,
+                                   float* spec, int wave, int lane, const int (&lo)[8], float* misc0,
+                                   float& theta_out) {
+    const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     float* wg_mm = reinterpret_cast<float*>(smem + L_WG + 16);   // [WAVES][2] max, min
     const int T = 1 + v.len / HOP;
-    const int ntile = (T + kFPP - 1) / kFPP;
+    const int ntile = (T + 15) >> 4;
     const int nloc = ntile > wave ? (ntile - wave + WAVES - 1) / WAVES : 0;
     const int col = lane & 15;
     double s1[8], s2[8];
@@ -511,36 +1287,38 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s1[i] = 0.0; s2[i] = 0.0; cref[i] = 0.0f; }
     float vmax = -INFINITY, vmin = INFINITY, nanp = 0.0f;
-    // the wave's last tile stays in registers (unclamped) until the segment max is known, so
-    // a segment of <= WAVES tiles (T <= 128) is never recomputed; earlier tiles are clamped
+    // the wave's last tile stays in LDS (unclamped) until the segment max is known, so a
+    // segment of <= WAVES tiles (T <= 128) is never recomputed; earlier tiles are clamped
     // speculatively at the running max (segment_stats) and recomputed if theta bites
     float run = -INFINITY, last_min = INFINITY;
-    float lm[32];
-    if (nloc > 0) stage_tile(v, wave, stage, lane);
     for (int lt = 0; lt < nloc; ++lt) {
         const int tile_i = wave + WAVES * lt;
         const bool last = lt + 1 == nloc;
         const bool rec = !last && lt < kSpecTiles;
         if (!rec) run = -INFINITY;
         float tmin = INFINITY;
-        stage_wait();
-        fp4::pass(tabs, stage, lane, tile_i * kFPP + col < T, lm, vmax, tmin, nanp, [&] {
-            if (!last) stage_tile(v, tile_i + WAVES, stage, lane);
-        });
+        tile_passes(v, tile_i, T, smem, scr, tile, lane, lo, vmax, tmin, nanp, run);
         const float tmw = wave_min(tmin);
         vmin = fminf(vmin, tmw);
         if (last) { last_min = tmw; break; }
         const float run2 = rec ? wave_max(vmax) - kTopDbUnits : -INFINITY;
+        if (run2 > run && tmw < run2) {   // self-clamp (segment_stats)
+            uint4 h[4], l[4];
+            clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
+            clamp_store(tile, lane, h, l, run2);
+            lds_order();
+        }
         run = fmaxf(run, run2);
         float c[8];
-        fp4::dct(lm, run, tabs, lane, c);
+        tile_dct(tile, s_dct, lane, c);
         if (lt == 0) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
         }
-        stats_add(c, cref, tile_i * kFPP + col < T, s1, s2);
-        if (lane == 0 && rec) {
-            spec[lt] = fmaxf(tmw, run);
+        stats_add(c, cref, tile_i * 16 + col < T, s1, s2);
+        if (lane == 0 && rec) {   // tile-granular records (both passes recomputed when theta bites)
+#pragma unroll
+            for (int p = 0; p < kPassesPerTile; ++p) spec[kPassesPerTile * lt + p] = fmaxf(tmw, run);
             spec[kSpecRun + lt] = run;
         }
     }
@@ -551,23 +1329,28 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
     for (int w = 0; w < WAVES; ++w) { vmax = fmaxf(vmax, wg_mm[2 * w]); vmin = fminf(vmin, wg_mm[2 * w + 1]); }
     const float theta = vmax - kTopDbUnits;
     theta_out = theta;
-    (void)last_min;
     if (nloc > 0) {
         const int tile_l = wave + WAVES * (nloc - 1);
+        if (last_min < theta) {   // the last tile, still in LDS: clamp at the final threshold
+            uint4 h[4], l[4];
+            clamp_load(reinterpret_cast<const float4*>(tile), lane, h, l);
+            clamp_store(tile, lane, h, l, theta);
+            lds_order();
+        }
         float c[8];
-        fp4::dct(lm, theta, tabs, lane, c);   // the last tile, still in registers: clamped at the final threshold
+        tile_dct(tile, s_dct, lane, c);
         if (nloc == 1) {
 #pragma unroll
             for (int i = 0; i < 8; ++i) cref[i] = __shfl(c[i], lane & 48, 64);
         }
-        stats_add(c, cref, tile_l * kFPP + col < T, s1, s2);
+        stats_add(c, cref, tile_l * 16 + col < T, s1, s2);
         if (vmin < theta) {
             lds_order();
             for (int lt = 0; lt + 1 < nloc; ++lt) {
                 const bool rec = lt < kSpecTiles;
-                if (rec && !(spec[lt] < theta)) continue;
-                fix_tile(v, wave + WAVES * lt, T, rec ? spec[kSpecRun + lt] : -INFINITY, theta, tabs, stage, lane, cref,
-                         s1, s2);
+                if (rec && !(spec[kPassesPerTile * lt] < theta)) continue;
+                fix_tile(v, wave + WAVES * lt, T, rec ? spec[kSpecRun + lt] : -INFINITY, theta, smem, scr, tile,
+                         lane, lo, cref, s1, s2);
             }
         }
     }
@@ -576,6 +1359,7 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
         for (int i = 0; i < 8; ++i) s1[i] = __builtin_nan("");
     }
     // this wave's per-coefficient (s1, s2, cref) -> its scratch, as doubles [coef][3]
+    double* pd = reinterpret_cast<double*>(scr);
 #pragma unroll
     for (int i = 0; i < 8; ++i) { s1[i] = row_sum_d(s1[i]); s2[i] = row_sum_d(s2[i]); }
     if (col == 15) {
@@ -594,14 +1378,14 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
     if (wave == 0) {
         double mean = 0.0, sd = 0.0;
         if (lane < NMFCC) {
-            const double* p0 = reinterpret_cast<const double*>(smem + L_WAVES + W_PD);
+            const double* p0 = reinterpret_cast<const double*>(smem + L_SCR);
             const double r0 = p0[3 * lane + 2];
             double S1 = 0.0, S2 = 0.0;
             for (int w = 0; w < WAVES; ++w) {
                 int n = 0;   // valid frames of wave w's tiles
-                for (int ti = w; ti < ntile; ti += WAVES) n += min(kFPP, T - kFPP * ti);
+                for (int ti = w; ti < ntile; ti += WAVES) n += min(16, T - 16 * ti);
                 if (n == 0) continue;
-                const double* pw = reinterpret_cast<const double*>(smem + L_WAVES + w * W_BYTES + W_PD);
+                const double* pw = reinterpret_cast<const double*>(smem + L_SCR + w * SCR_BYTES);
                 const double a1 = pw[3 * lane], a2 = pw[3 * lane + 1], d = pw[3 * lane + 2] - r0;
                 S1 += a1 + (double)n * d;
                 S2 += a2 + 2.0 * d * a1 + (double)n * d * d;
@@ -787,8 +1571,61 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
         // a quiet tick's 256 workgroups)
         if (MODE == 1 && (int)blockIdx.x >= r_count) return;   // (k_rescore_ring ends the tick)
     }
-    // ---- cooperative table load (global -> LDS)
-    fp4::fill_tables(tab, smem + L_TAB, kWinScale, threadIdx.x, blockDim.x);
+    // ---- cooperative table load (global -> LDS), per-lane rows transposed
+    {
+        float2* sw2 = reinterpret_cast<float2*>(smem + L_WIN2);
+        float2* st1 = reinterpret_cast<float2*>(smem + L_TW1);
+        float2* st2 = reinterpret_cast<float2*>(smem + L_TW2);
+        for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+            const int j = i & 15, n = i >> 4;   // win2[16n + j], tw1[16n + j], tw2[j + 16n]
+            sw2[j * TP + n] = make_float2(tab->win2[i].x * kWinScale, tab->win2[i].y * kWinScale);
+            if (n > 0) st1[j * TP + n - 1] = tab->tw1[i];
+        }
+        // [j'][it] = (cos, tan) of tw2[k] for the bin k that lane class j' untangles at step it
+        for (int i = threadIdx.x; i < 8 * 17; i += blockDim.x) {
+            const int jp = i / 17, it = i % 17;
+            const int k = jp ? jp + 16 * (it < 16 ? it : 15) : (it <= 8 ? 16 * it : 8 + 16 * (it - 9));
+            const float2 cs = tab->tw2[k];   // (c, t): c = cos is never 0 in float (k = 128: 6.1e-17)
+            st2[jp * TP + it] = make_float2(cs.x, cs.y / cs.x);
+        }
+        int* sb = reinterpret_cast<int*>(smem + L_BLO);
+        for (int i = threadIdx.x; i < NMEL; i += blockDim.x) sb[i] = tab->band_lo[i];
+        float* sw = reinterpret_cast<float*>(smem + L_WPAD);
+        for (int i = threadIdx.x; i < 16 * WP; i += blockDim.x) {
+            const int j = i / WP, o = i % WP;
+            float w = 0.0f;
+#pragma unroll
+            for (int g = 0; g < 8; ++g)
+                if (o >= kMelOff[g] && o < kMelOff[g] + kMelW[g]) w = tab->wpad[(kMelIt0[g] + o - kMelOff[g]) * 16 + j];
+            sw[i] = w;
+        }
+        // the f16 hi/lo DCT operand chunks (kDctScale keeps the lo parts normal)
+        uint4* sd = reinterpret_cast<uint4*>(smem + L_DCT);
+        for (int i = threadIdx.x; i < DCT_BYTES / 16; i += blockDim.x) {
+            int row = -1, c = 0, hl = 0;
+            if (i < DCT_RT1 / 16) {
+                const int l = i & 63;
+                hl = (i >> 6) & 1;
+                row = l & 15;
+                c = 4 * (i >> 7) + (l >> 4);
+            } else {
+                const int k = i - DCT_RT1 / 16, blk = k / 17, slot = k % 17;   // blk = q * 2 + hl
+                if (slot < 16) {
+                    row = 16 + (slot & 3);
+                    c = 4 * (blk >> 1) + (slot >> 2);
+                    hl = blk & 1;
+                }
+            }
+            float v[8];
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+                const float d = row >= 0 ? tab->dct[row * NMEL + c + 16 * jj] * kDctScale : 0.0f;
+                const float h = f16_trunc(d);
+                v[jj] = hl ? d - h : h;
+            }
+            sd[i] = make_uint4(pk_f16(v[0], v[1]), pk_f16(v[2], v[3]), pk_f16(v[4], v[5]), pk_f16(v[6], v[7]));
+        }
+    }
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int base = 0, count = a.n_seg;
@@ -796,11 +1633,16 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
         base = r_base;
         count = r_count;
     }
-    // the wave's LDS (a wave-uniform base: the LDS-DMA destination lives in M0)
-    unsigned char* wbase = smem + L_WAVES + __builtin_amdgcn_readfirstlane(wave * W_BYTES);
-    float* stage = reinterpret_cast<float*>(wbase + W_STAGE);
-    double* pd = reinterpret_cast<double*>(wbase + W_PD);
+    unsigned char* wbase = smem + L_SHARED_END + wave * W_BYTES;
+    float* scr = reinterpret_cast<float*>(smem + L_SCR + wave * SCR_BYTES);
+    float* tile = reinterpret_cast<float*>(wbase + W_TILE);
     float* spec = reinterpret_cast<float*>(wbase + W_SPEC);
+    int lo[8];   // first bin of this lane's bands j + 16 i
+    {
+        const int* sb = reinterpret_cast<const int*>(smem + L_BLO);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) lo[i] = sb[(lane & 15) + 16 * i];
+    }
     // persistent waves pull segments from a work counter (ragged lengths balance)
     // the template is loop-invariant: fetched once, off every segment's critical path.
     // (Reserving the next work item ahead was tried: the tail imbalance costs more.)
@@ -813,7 +1655,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
     // take whole segments from the work counter, like a linear batch.
     if (MODE == 1) {
         int* wg_idx = reinterpret_cast<int*>(smem + L_WG);
-        float* misc0 = reinterpret_cast<float*>(smem + L_WAVES + W_PD);   // wave 0's scratch (epilogue only)
+        float* misc0 = reinterpret_cast<float*>(smem + L_SCR);   // wave 0's FFT scratch (epilogue only)
         // first segment by workgroup index (its event was requested before the table fill),
         // later ones from the work counter (a burst tick's segments balance over the grid)
         for (int idx = blockIdx.x; idx < count;) {
@@ -828,7 +1670,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
                     static_cast<const unsigned char*>(ring_base) + (int64_t)ev.stream * a.ring_len * sample_bytes(RING),
                     ev.ring_start, a.ring_len, ev.length);
                 float theta_s;
-                segment_stats_coop(v, smem, stage, spec, pd, wave, lane, misc0, theta_s);
+                segment_stats_coop(v, smem, scr, tile, spec, wave, lane, lo, misc0, theta_s);
                 if (wave == 0 && (a.has_template || a.list_all))
                     score_epilogue<RING>(a, act ? misc0[lane] : 0.0f, act ? misc0[20 + lane] : 0.0f, tmf, tsf, lane,
                                          seg, v.len, theta_s);
@@ -869,7 +1711,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
 
         double st1[8], st2[8];
         float theta_s;
-        segment_stats(v, smem + L_TAB, stage, spec, pd, lane, st1, st2, theta_s, wc, nx EWK_DBG_ARG);
+        segment_stats(v, smem, scr, tile, spec, lane, lo, st1, st2, theta_s, wc, nx EWK_DBG_ARG);
         EWK_TS(tw2);
 
         // ---- lane k < 20 holds coefficient k's mean / std (fp32-rounded like the reference's)
