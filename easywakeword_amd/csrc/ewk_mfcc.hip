@@ -1744,6 +1744,12 @@ extern "C" int ewk_debug_rs(unsigned long long* out) {   // read and reset (debu
     if (hipMemcpyToSymbol(HIP_SYMBOL(ewk::g_rs_dbg), z, sizeof(z)) != hipSuccess) return -3;
     return 0;
 }
+extern "C" int ewk_debug_rs_ph(unsigned long long* out) {   // chunk sub-phase cycles (debug builds only)
+    unsigned long long z[8] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ewk::g_rs_ph), sizeof(z)) != hipSuccess) return -3;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(ewk::g_rs_ph), z, sizeof(z)) != hipSuccess) return -3;
+    return 0;
+}
 namespace ewk {
 #endif
 

@@ -37,8 +37,16 @@
 #ifdef EWK_RS_TIMING
 __device__ unsigned long long g_rs_dbg[16];
 #define EWK_RS_ADD(k, v) (void)atomicAdd(&g_rs_dbg[k], (unsigned long long)(v))
+// chunk sub-phases (s_memtime cycles summed over chunks): 0 samples + window, 1 FFT stages,
+// 2 untangle + power, 3 mel + log10, 4 DCT, 5 sums + flags, 6 chunks, 7 frame groups
+__device__ unsigned long long g_rs_ph[8];
+#define EWK_RS_TS(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define EWK_RS_PH(k, a, b) \
+    do { if (lane == 0) (void)atomicAdd(&g_rs_ph[k], (unsigned long long)((b) - (a))); } while (0)
 #else
 #define EWK_RS_ADD(k, v) ((void)0)
+#define EWK_RS_TS(v)
+#define EWK_RS_PH(k, a, b) ((void)0)
 #endif
 
 constexpr double kRsWindow = 1e-3;   // dB; the float32 max is within ~1e-5 dB of the fp64 one
@@ -98,11 +106,14 @@ constexpr int RS_MOFF = RS_MLO + NMEL * 4;                  // int [NMEL + 1]
 constexpr int RS_MW = RS_MOFF + (NMEL + 4) * 4;             // float [2 NBIN + 2 NMEL]
 constexpr int RS_MW_N = 2 * NBIN + 2 * NMEL;
 constexpr int RS_WAVES = (RS_MW + RS_MW_N * 4 + 15) & ~15;
-constexpr int RS_BUF = 0;                                   // per wave: double2 [256] FFT / double P[257]
-constexpr int RS_XA = 256 * 16;                             // double [NMEL][kRsFrames]: the chunk's log-mel
+// Two frames in flight per wave (rs_frames): each has its own FFT buffer.
+constexpr int RS_NF = 2;
+constexpr int RS_BUF = 0;                                   // per wave: RS_NF x (double2 [256] FFT / double P[257])
+constexpr int RS_XA = RS_NF * 256 * 16;                     // double [NMEL][kRsFrames]: the chunk's log-mel
 constexpr int RS_WAVE_BYTES = RS_XA + NMEL * kRsFrames * 8;
 constexpr int RS_FLAGS = RS_WAVES + RS_NW * RS_WAVE_BYTES;  // int [3 + RS_NW]: score_tail's flags
-constexpr int RS_LDS = RS_FLAGS + 4 * (3 + RS_NW);
+constexpr int RS_PRE = (RS_FLAGS + 4 * (3 + RS_NW) + 15) & ~15;   // TickPre (empty-launch tick end)
+constexpr int RS_LDS = RS_PRE + 32;
 static_assert(RS_LDS <= 160 * 1024, "the re-score workgroup must fit a CU's LDS");
 static_assert(NMFCC == 20 && kRsFrames == 8, "the DCT lane split assumes 20 coefficients and 8-frame chunks");
 
@@ -240,62 +251,95 @@ __device__ __forceinline__ void rs_window(const float (&smp)[8], const RsLane& c
     for (int r = 0; r < 4; ++r) x[r] = make_double2(c.win[2 * r] * (double)smp[2 * r], c.win[2 * r + 1] * (double)smp[2 * r + 1]);
 }
 
-__device__ __forceinline__ void rs_frame(const double2 (&xw)[4], const RsLane& c, unsigned char* wbuf,
-                                         const unsigned char* smem, int lane, int f, double theta_s, double W,
-                                         double& mx, bool& amb, bool& nanf, bool& clp) {
-    double2* buf = reinterpret_cast<double2*>(wbuf + RS_BUF);
-    double2 x[4];
+// FFT buffer slot of complex element i (16-B units): the low 4 bits XORed with 5 x (i >> 4).
+// Every radix-4 Stockham store (slot ((j >> lg) << (lg + 2)) + j % 4^lg + r 4^lg) and every
+// natural-order read then hits 16 distinct 16-B bank groups per 16 lanes (unswizzled, the Ns = 1
+// and 4 stores were 4-way conflicts: 41 % of the launch's LDS cycles).  scripts/f64_chunk_model.py
+// checks the permutation and the conflict counts.
+__device__ __forceinline__ int rs_swz(int i) { return i ^ (((i >> 4) * 5) & 15); }
+
+// NF frames f0 .. f0 + NF - 1 (samples already windowed) -> columns f0 .. of the chunk's
+// log-mel tile, interleaved: the frames' FFT stages, untangles and bands are independent
+// instruction streams, so one frame's LDS round trips and fp64 latencies overlap the other's
+// (one frame at a time, a chunk waited 70 % of its cycles).  valid[j]: frame j counts towards
+// mx / amb / nanf / clp (a chunk's odd last frame rides along as a dummy).
+template <int NF>
+__device__ __forceinline__ void rs_frames(const double2 (&xw)[NF][4], const bool (&valid)[NF], const RsLane& c,
+                                          unsigned char* wbuf, const unsigned char* smem, int lane, int f0,
+                                          double theta_s, double W, double& mx, bool& amb, bool& nanf, bool& clp) {
+    EWK_RS_TS(p0);
+    double2 x[NF][4];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) x[r] = xw[r];
+    for (int j = 0; j < NF; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[j][r] = xw[j][r];
     // radix-4 Stockham autosort: v[r] = d[j + 64 r], v[r] *= W_{4 Ns}^{r (j % Ns)}, DFT4,
     // V[r] -> d'[(j / Ns) 4 Ns + j % Ns + r Ns]; natural order after Ns = 64
-#pragma unroll
 #ifndef EWK_RS_SKIP_FFT
     for (int it = 0; it < 4; ++it) {
 #else
     for (int it = 0; it < 4; it += 3) {
 #endif
-        if (it > 0) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) x[r] = buf[lane + 64 * r];
+        for (int j = 0; j < NF; ++j) {
+            double2* buf = reinterpret_cast<double2*>(wbuf + RS_BUF) + 256 * j;
+            if (it > 0) {
 #pragma unroll
-            for (int r = 1; r < 4; ++r) x[r] = zmul(x[r], c.tw[3 * (it - 1) + r - 1]);
+                for (int r = 0; r < 4; ++r) x[j][r] = buf[rs_swz(lane + 64 * r)];
+#pragma unroll
+                for (int r = 1; r < 4; ++r) x[j][r] = zmul(x[j][r], c.tw[3 * (it - 1) + r - 1]);
+            }
+            const double2 a0 = make_double2(x[j][0].x + x[j][2].x, x[j][0].y + x[j][2].y);
+            const double2 a1 = make_double2(x[j][0].x - x[j][2].x, x[j][0].y - x[j][2].y);
+            const double2 a2 = make_double2(x[j][1].x + x[j][3].x, x[j][1].y + x[j][3].y);
+            const double2 a3 = make_double2(x[j][1].x - x[j][3].x, x[j][1].y - x[j][3].y);
+            x[j][0] = make_double2(a0.x + a2.x, a0.y + a2.y);
+            x[j][2] = make_double2(a0.x - a2.x, a0.y - a2.y);
+            x[j][1] = make_double2(a1.x + a3.y, a1.y - a3.x);   // a1 - i a3
+            x[j][3] = make_double2(a1.x - a3.y, a1.y + a3.x);   // a1 + i a3
         }
-        const double2 a0 = make_double2(x[0].x + x[2].x, x[0].y + x[2].y);
-        const double2 a1 = make_double2(x[0].x - x[2].x, x[0].y - x[2].y);
-        const double2 a2 = make_double2(x[1].x + x[3].x, x[1].y + x[3].y);
-        const double2 a3 = make_double2(x[1].x - x[3].x, x[1].y - x[3].y);
-        x[0] = make_double2(a0.x + a2.x, a0.y + a2.y);
-        x[2] = make_double2(a0.x - a2.x, a0.y - a2.y);
-        x[1] = make_double2(a1.x + a3.y, a1.y - a3.x);   // a1 - i a3
-        x[3] = make_double2(a1.x - a3.y, a1.y + a3.x);   // a1 + i a3
         const int lg = 2 * it;
         const int base = it < 3 ? ((lane >> lg) << (lg + 2)) + (lane & ((1 << lg) - 1)) : lane;
         wave_sync();   // every lane has read this iteration's inputs
 #pragma unroll
-        for (int r = 0; r < 4; ++r) buf[base + (r << lg)] = x[r];   // (it = 3: Z[lane + 64 r])
+        for (int j = 0; j < NF; ++j) {
+            double2* buf = reinterpret_cast<double2*>(wbuf + RS_BUF) + 256 * j;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) buf[rs_swz(base + (r << lg))] = x[j][r];   // (it = 3: Z[lane + 64 r])
+        }
         wave_sync();
     }
+    EWK_RS_TS(p1);
+    EWK_RS_PH(1, p0, p1);
     // untangle: X[k] = E + W512^k O,  E = (Z[k] + conj Z[256-k]) / 2,  O = (Z[k] - conj Z[256-k]) / 2i
-    double p[4];
+    double p[NF][4], d256[NF];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int k = lane + 64 * r;
-        const double2 zk = x[r], zc = buf[(256 - k) & 255];
-        const double er = 0.5 * (zk.x + zc.x), ei = 0.5 * (zk.y - zc.y);
-        const double orr = 0.5 * (zk.y + zc.y), oi = -0.5 * (zk.x - zc.x);
-        const double2 cs = c.tu[r];
-        const double xr = er + (orr * cs.x + oi * cs.y);
-        const double xi = ei + (oi * cs.x - orr * cs.y);
-        p[r] = xr * xr + xi * xi;
+    for (int j = 0; j < NF; ++j) {
+        const double2* buf = reinterpret_cast<const double2*>(wbuf + RS_BUF) + 256 * j;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int k = lane + 64 * r;
+            const double2 zk = x[j][r], zc = buf[rs_swz((256 - k) & 255)];
+            const double er = 0.5 * (zk.x + zc.x), ei = 0.5 * (zk.y - zc.y);
+            const double orr = 0.5 * (zk.y + zc.y), oi = -0.5 * (zk.x - zc.x);
+            const double2 cs = c.tu[r];
+            const double xr = er + (orr * cs.x + oi * cs.y);
+            const double xi = ei + (oi * cs.x - orr * cs.y);
+            p[j][r] = xr * xr + xi * xi;
+        }
+        d256[j] = x[j][0].x - x[j][0].y;   // k = 256 (lane 0): W512^256 = -1 exactly
     }
-    const double d256 = x[0].x - x[0].y;   // k = 256 (lane 0): W512^256 = -1 exactly
     wave_sync();
-    double* P = reinterpret_cast<double*>(buf);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) P[lane + 64 * r] = p[r];
-    if (lane == 0) P[256] = d256 * d256;
+    for (int j = 0; j < NF; ++j) {
+        double* P = reinterpret_cast<double*>(wbuf + RS_BUF) + 512 * j;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) P[lane + 64 * r] = p[j][r];
+        if (lane == 0) P[256] = d256[j] * d256[j];
+    }
     wave_sync();
+    EWK_RS_TS(p2);
+    EWK_RS_PH(2, p1, p2);
     // mel (every non-zero weight of the band, in bin order) + dB; lane: bands lane, 127 - lane
     const int* mlo = reinterpret_cast<const int*>(smem + RS_MLO);
     const int* moff = reinterpret_cast<const int*>(smem + RS_MOFF);
@@ -308,37 +352,45 @@ __device__ __forceinline__ void rs_frame(const double2 (&xw)[4], const RsLane& c
     for (int h = 0; h < 2; ++h) {
         const int m = h ? NMEL - 1 - lane : lane;
         const int lo = mlo[m], o0 = moff[m], nw = moff[m + 1] - o0;
-        double pw[kRsMelW];
         float ww[kRsMelW];
 #pragma unroll
-        for (int q = 0; q < kRsMelW; ++q) {
-            ww[q] = q < nw ? mw[min(o0 + q, RS_MW_N - 1)] : 0.0f;
-            pw[q] = P[lo + q];   // lo + q < 2 * 256: inside the wave's FFT buffer
-        }
-        double acc = 0.0;
-#ifndef EWK_RS_SKIP_MEL
-        // past the band: weight 0 times a finite power of this frame (its FFT buffer; a NaN
-        // there means NaN samples, and then every bin is NaN) adds +-0, and acc + -0 = acc
+        for (int q = 0; q < kRsMelW; ++q) ww[q] = q < nw ? mw[min(o0 + q, RS_MW_N - 1)] : 0.0f;
 #pragma unroll
-        for (int q = 0; q < kRsMelW; ++q) acc = fma((double)ww[q], pw[q], acc);
+        for (int j = 0; j < NF; ++j) {
+            const double* P = reinterpret_cast<const double*>(wbuf + RS_BUF) + 512 * j;
+            double pw[kRsMelW];
+#pragma unroll
+            for (int q = 0; q < kRsMelW; ++q) pw[q] = P[lo + q];   // lo + q < 2 * 256: inside the frame's buffer
+            double acc = 0.0;
+#ifndef EWK_RS_SKIP_MEL
+            // past the band: weight 0 times a finite power of this frame (its FFT buffer; a NaN
+            // there means NaN samples, and then every bin is NaN) adds +-0, and acc + -0 = acc
+#pragma unroll
+            for (int q = 0; q < kRsMelW; ++q) acc = fma((double)ww[q], pw[q], acc);
 #else   // (timing experiment: one bin per band)
-        acc = pw[0] + (double)ww[0] + (double)nw;
+            acc = pw[0] + (double)ww[0] + (double)nw;
 #endif
 #ifndef EWK_RS_SKIP_LOG
-        const double db = 10.0 * log10(acc < 1e-10 ? 1e-10 : acc);   // np.maximum: NaN propagates
+            const double db = 10.0 * log10(acc < 1e-10 ? 1e-10 : acc);   // np.maximum: NaN propagates
 #else
-        const double db = acc;
+            const double db = acc;
 #endif
-        // the A operand, or -0.0 for a value the clamp replaces (NaN included): fma(d, -0, A) = A
-        // as with +0, and db is never -0.0 (10 log10(acc), acc >= 1e-10), so -0.0 also marks
-        // the B operand for rs_dct (no second tile)
-        xa[m * kRsFrames + f] = db >= theta_s ? db : -0.0;
-        clp = clp || !(db >= theta_s);
-        mx = fmax(mx, db);
-        amb = amb || fabs(db - theta_s) <= W;
-        nanf = nanf || db != db;
+            // the A operand, or -0.0 for a value the clamp replaces (NaN included): fma(d, -0, A) = A
+            // as with +0, and db is never -0.0 (10 log10(acc), acc >= 1e-10), so -0.0 also marks
+            // the B operand for rs_dct (no second tile)
+            xa[m * kRsFrames + f0 + j] = db >= theta_s ? db : -0.0;
+            if (valid[j]) {
+                clp = clp || !(db >= theta_s);
+                mx = fmax(mx, db);
+                amb = amb || fabs(db - theta_s) <= W;
+                nanf = nanf || db != db;
+            }
+        }
     }
     wave_sync();
+    EWK_RS_TS(p3);
+    EWK_RS_PH(3, p2, p3);
+    EWK_RS_PH(7, 0ull, 1ull);
 }
 
 // DCT of the chunk's n frames split at theta_s: lane k < 20 returns A_k, B_k of frames 0..7
@@ -419,22 +471,39 @@ __device__ void rs_chunk(const RsSrc<RING>& v, int T, int c, double theta_s, dou
     n = min(kRsFrames, T - t0);
     double m = -INFINITY;
     bool amb = false, nanf = false, clp = false;
-    float smp[8];
-    rs_load(v, t0, lane, smp);
-    for (int f = 0; f < n; ++f) {
-        double2 xw[4];
-        rs_window(smp, cl, xw);
-        // the next frame's loads go out only after this frame's samples are consumed (issued
-        // before, the compiler's in-order vmcnt wait for this frame's samples also covered the
-        // first of them; time-neutral, profiles/r04_v9_rescore_pmc.txt)
-        asm volatile("" ::"v"(xw[0].x), "v"(xw[0].y), "v"(xw[1].x), "v"(xw[1].y), "v"(xw[2].x), "v"(xw[2].y),
-                     "v"(xw[3].x), "v"(xw[3].y)
-                     : "memory");
-        if (f + 1 < n) rs_load(v, t0 + f + 1, lane, smp);
-        rs_frame(xw, cl, wbuf, smem, lane, f, theta_s, W, m, amb, nanf, clp);
+    float smp[RS_NF][8];
+#pragma unroll
+    for (int j = 0; j < RS_NF; ++j) rs_load(v, t0 + j, lane, smp[j]);   // (past T: range-checked zeros)
+    for (int f = 0; f < n; f += RS_NF) {
+        EWK_RS_TS(w0);
+        double2 xw[RS_NF][4];
+        bool valid[RS_NF];
+#pragma unroll
+        for (int j = 0; j < RS_NF; ++j) {
+            rs_window(smp[j], cl, xw[j]);
+            valid[j] = f + j < n;
+        }
+        // the next frames' loads go out only after these frames' samples are consumed (issued
+        // before, the compiler's in-order vmcnt wait for these samples also covered the first
+        // of them; time-neutral, profiles/r04_v9_rescore_pmc.txt)
+#pragma unroll
+        for (int j = 0; j < RS_NF; ++j)
+            asm volatile("" ::"v"(xw[j][0].x), "v"(xw[j][0].y), "v"(xw[j][1].x), "v"(xw[j][1].y), "v"(xw[j][2].x),
+                         "v"(xw[j][2].y), "v"(xw[j][3].x), "v"(xw[j][3].y)
+                         : "memory");
+        EWK_RS_TS(w1);
+        EWK_RS_PH(0, w0, w1);
+        if (f + RS_NF < n) {
+#pragma unroll
+            for (int j = 0; j < RS_NF; ++j) rs_load(v, t0 + f + RS_NF + j, lane, smp[j]);
+        }
+        rs_frames<RS_NF>(xw, valid, cl, wbuf, smem, lane, f, theta_s, W, m, amb, nanf, clp);
     }
     double A[8], B[8];
+    EWK_RS_TS(d0);
     rs_dct(smem, wbuf, lane, __ballot(clp) != 0, A, B);
+    EWK_RS_TS(d1);
+    EWK_RS_PH(4, d0, d1);
     const double rA = A[0], rB = B[0];
     double sA = 0.0, sB = 0.0, sAA = 0.0, sAB = 0.0, sBB = 0.0;
 #pragma unroll
@@ -451,6 +520,9 @@ __device__ void rs_chunk(const RsSrc<RING>& v, int T, int c, double theta_s, dou
     pv[0] = rA; pv[1] = rB; pv[2] = sA; pv[3] = sB; pv[4] = sAA; pv[5] = sAB; pv[6] = sBB;
     mx = wave_max_d(m);
     flags = (__ballot(amb) ? 1 : 0) | (__ballot(nanf) ? 2 : 0);
+    EWK_RS_TS(d2);
+    EWK_RS_PH(5, d1, d2);
+    EWK_RS_PH(6, 0ull, 1ull);
 }
 
 // Chunk sums merged in chunk order as polynomials in theta (the clamp is known only at the end):
@@ -741,19 +813,26 @@ __device__ __forceinline__ bool rs_pending(const RsArgs& a) {
 
 // The end of a scoring pass (one workgroup, after the list is drained): re-arm the counters
 // for the next launch, advance the event watermark (ring mode) and write the poll mirror.
+// pre (empty launch, thread 0 of workgroup 0): the event count and the bank's counters, loaded
+// at the launch's start together with the list count (three dependent round trips -> one); with
+// no re-score write to publish, the counters need no fence (the launch's end releases them).
+struct TickPre {
+    int32_t n_events;
+    uint4 c;
+};
 template <int RING>
-__device__ void tick_end(const ScoreArgs& a) {
+__device__ void tick_end(const ScoreArgs& a, const TickPre* pre = nullptr) {
     if (threadIdx.x == 0) {
-        if (RING) *a.adv_ev_base = *a.n_events;
+        if (RING) *a.adv_ev_base = pre ? pre->n_events : *a.n_events;
         *a.work = 0;
 #pragma unroll
         for (int i = 0; i < kRsCtl; ++i) a.rs_ctl[i] = 0;
-        __threadfence();
+        if (!pre) __threadfence();
     }
     if (RING && a.mirror) {   // poll mirror: the bank's counters and first events -> pinned host memory
         __syncthreads();   // this workgroup's re-score writes are done and fenced by thread 0
         const volatile int32_t* vc = a.evc;
-        const uint4 c = make_uint4((uint32_t)vc[0], (uint32_t)vc[1], (uint32_t)vc[2], (uint32_t)vc[3]);
+        const uint4 c = pre ? pre->c : make_uint4((uint32_t)vc[0], (uint32_t)vc[1], (uint32_t)vc[2], (uint32_t)vc[3]);
         const int32_t n = (int32_t)min(min((uint32_t)(c.x - (uint32_t)a.ev_base0), (uint32_t)a.n_seg),
                                        (uint32_t)a.mirror_chunk);
         if (threadIdx.x == 0) *reinterpret_cast<uint4*>(a.mirror) = c;
@@ -779,11 +858,25 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem) {
     int* flag = reinterpret_cast<int*>(smem + RS_FLAGS);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const RsArgs ra = rs_args(a);
-    if (threadIdx.x == 0)
+    TickPre* pre = reinterpret_cast<TickPre*>(smem + RS_PRE);
+    if (threadIdx.x == 0) {
+        // (workgroup 0 also requests what the tick end needs, in the same round trip)
+        int32_t ne = 0;
+        uint4 c = make_uint4(0, 0, 0, 0);
+        if (RING && blockIdx.x == 0) {
+            ne = *a.n_events;
+            if (a.mirror) {
+                const volatile int32_t* vc = a.evc;
+                c = make_uint4((uint32_t)vc[0], (uint32_t)vc[1], (uint32_t)vc[2], (uint32_t)vc[3]);
+            }
+        }
         flag[2 + RS_NW] = a.rs_slots ? __hip_atomic_load(&a.rs_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        pre->n_events = ne;
+        pre->c = c;
+    }
     __syncthreads();
     if (flag[2 + RS_NW] == 0) {   // nothing listed: the list stays empty for this launch
-        if (blockIdx.x == 0) tick_end<RING>(a);
+        if (blockIdx.x == 0) tick_end<RING>(a, RING ? pre : nullptr);
         return;
     }
     bool loaded = false, finished = false;

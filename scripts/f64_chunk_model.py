@@ -97,6 +97,31 @@ def model_stats(x, theta_s, W=1e-3, F=8):
     return mean, np.sqrt(var), recomputed
 
 
+def rs_swz(i):
+    """FFT buffer slot of complex element i (ewk_rescore.h rs_swz)."""
+    return i ^ (((i >> 4) * 5) & 15)
+
+
+def swizzle_conflicts():
+    """Worst bank-group multiplicity of each 16-lane group's 16-B accesses (1 = conflict free)
+    for the Stockham stores, the natural-order reads and the untangle's partner reads, with and
+    without rs_swz; also checks that rs_swz permutes 0..255."""
+    from collections import Counter
+    assert sorted(rs_swz(i) for i in range(256)) == list(range(256))
+
+    def worst(addrs):
+        return max(max(Counter(a % 16 for a in addrs[16 * q:16 * q + 16]).values()) for q in range(4))
+
+    out = {}
+    for name, f in (("plain", lambda i: i), ("swizzled", rs_swz)):
+        st = max(worst([f((((l >> lg) << (lg + 2)) + (l & ((1 << lg) - 1)) if lg < 6 else l) + (r << lg))
+                        for l in range(64)]) for lg in (0, 2, 4, 6) for r in range(4))
+        rd = max(worst([f(l + 64 * r) for l in range(64)]) for r in range(4))
+        un = max(worst([f((256 - (l + 64 * r)) & 255) for l in range(64)]) for r in range(4))
+        out[name] = {"stores": st, "reads": rd, "untangle_reads": un}
+    return out
+
+
 if __name__ == "__main__":
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests"))
     import synth

@@ -31,6 +31,8 @@ dbg = hasattr(dlib, "ewk_debug_rs")
 dbuf = (ctypes.c_ulonglong * 16)()
 if dbg:
     dlib.ewk_debug_rs(dbuf)
+    if hasattr(dlib, "ewk_debug_rs_ph"):
+        dlib.ewk_debug_rs_ph((ctypes.c_ulonglong * 8)())
 rows = []
 for i in range(ticks):
     k = t % period
@@ -54,6 +56,15 @@ for i in range(ticks):
     T = 1 + rs["length"].astype(np.int64) // 160
     rows.append((len(real), len(rs), int(T.sum()), int(((T + 7) // 8).sum()), int(T.max()) if len(T) else 0, sc_ms * 1e3, r_ms * 1e3))
     t += 1
+if dbg and hasattr(dlib, "ewk_debug_rs_ph"):
+    ph = (ctypes.c_ulonglong * 8)()
+    dlib.ewk_debug_rs_ph(ph)   # (accumulated over all timed ticks; the prefill's were reset above)
+    ph = list(ph)
+    nch, ngr = max(1, ph[6]), max(1, ph[7])
+    print(f"chunk sub-phases over {ph[6]} chunks ({ph[7]} frame groups), s_memtime cycles per chunk: "
+          f"samples+window {ph[0] / nch:,.0f}  FFT {ph[1] / nch:,.0f}  untangle {ph[2] / nch:,.0f}  "
+          f"mel+log10 {ph[3] / nch:,.0f}  DCT {ph[4] / nch:,.0f}  sums+flags {ph[5] / nch:,.0f}  "
+          f"(total {sum(ph[:6]) / nch:,.0f})")
 a = np.array(rows, dtype=np.float64)
 print("tick events listed frames chunks maxT scorer_us rescore_us")
 for r in rows[:40]:
