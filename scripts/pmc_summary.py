@@ -80,7 +80,12 @@ def main():
         if len(sys.argv) > 3:
             import json
             with open(sys.argv[3], "w") as fh:
+                import datetime
                 json.dump({"kernel": "k_score_f32", "segments": n, "frames": frames,
+                           "head": os.environ.get("EWK_HEAD", "unknown"),
+                           "date_utc": datetime.datetime.utcnow().strftime("%Y-%m-%dT%H:%M:%SZ"),
+                           "valu_active_frac": (c["SQ_ACTIVE_INST_VALU"] * 4 / waves) / (c["SQ_WAVE_CYCLES"] * 4 / waves)
+                           if waves and "SQ_ACTIVE_INST_VALU" in c else None,
                            "fetch_bytes": fetch, "write_bytes": write, "traffic_bytes": fetch + write,
                            "traffic_bytes_per_frame": (fetch + write) / frames,
                            # wave-instructions per MFCC frame (bench.py's VALU-issue roofline)
