@@ -525,6 +525,24 @@ __device__ void rs_chunk(const RsSrc<RING>& v, int T, int c, double theta_s, dou
     EWK_RS_PH(6, 0ull, 1ull);
 }
 
+// A part record's fields cross waves (any XCD) inside one launch: they are stored and loaded as
+// agent-scope relaxed atomics (global_store / global_load with sc1: performed at the agent's
+// coherence point, no copy kept in a CU's vector L1 or an XCD's L2), so the hand-off does not
+// depend on the pool's memory type or on which records share a 128-B line.  The writer's
+// s_waitcnt vmcnt(0) (its stores acknowledged) precedes its done count; the finishing wave's
+// agent acquire (buffer_inv sc1) follows the count that made it last.  DESIGN.md, "fp64
+// re-score", hand-off.
+// (global address space: global_* instructions, counted by vmcnt alone, not flat_*)
+template <class T>
+__device__ __forceinline__ void rs_st(T* p, T v) {
+    __hip_atomic_store((__attribute__((address_space(1))) T*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ T rs_ld(const T* p) {
+    return __hip_atomic_load((__attribute__((address_space(1))) T*)const_cast<T*>(p), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Chunk sums merged in chunk order as polynomials in theta (the clamp is known only at the end):
 // S1(theta) = P1a + theta P1b, S2(theta) = P2a + theta P2b + theta^2 P2c around the first
 // chunk's first frame c_0(theta) = rA0 + theta rB0.
@@ -567,7 +585,7 @@ __device__ void rs_finish(const RsArgs& a, RsSlot* sp, int seg, int T, float the
         for (int c0 = 0; c0 < nch; c0 += 64) {
             double m = -INFINITY;
             int f = 0;
-            if (c0 + lane < nch) { m = parts[c0 + lane].mx; f = parts[c0 + lane].flags; }
+            if (c0 + lane < nch) { m = rs_ld(&parts[c0 + lane].mx); f = rs_ld(&parts[c0 + lane].flags); }
             mx = fmax(mx, wave_max_d(m));
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) f |= __shfl_xor(f, o, 64);
@@ -595,11 +613,11 @@ __device__ void rs_finish(const RsArgs& a, RsSlot* sp, int seg, int T, float the
         int nn = 0, nfl = 0;
         auto fetch = [&](int c) {
             if (parts && c < nch) {
-                nn = parts[c].n;
-                nfl = parts[c].flags;
+                nn = rs_ld(&parts[c].n);
+                nfl = rs_ld(&parts[c].flags);
                 if (lane < NMFCC) {
 #pragma unroll
-                    for (int q = 0; q < 7; ++q) nx[q] = parts[c].v[q * NMFCC + lane];
+                    for (int q = 0; q < 7; ++q) nx[q] = rs_ld(&parts[c].v[q * NMFCC + lane]);
                 }
             }
         };
@@ -768,13 +786,14 @@ __device__ __attribute__((noinline)) bool rs_drain(const RsArgs& a, unsigned cha
         RsPart* pp = a.rs_parts + base + unit;
         if (lane < NMFCC) {
 #pragma unroll
-            for (int q = 0; q < 7; ++q) pp->v[q * NMFCC + lane] = pv[q];
+            for (int q = 0; q < 7; ++q) rs_st(&pp->v[q * NMFCC + lane], pv[q]);
         }
-        if (lane == 0) { pp->mx = mx; pp->n = n; pp->flags = flags; }
+        if (lane == 0) { rs_st(&pp->mx, mx); rs_st(&pp->n, n); rs_st(&pp->flags, flags); }
 #ifdef EWK_RS_TIMING
         if (lane == 0) { EWK_RS_ADD(1, 1); EWK_RS_ADD(2, __builtin_amdgcn_s_memrealtime() - c0); }
 #endif
-        // the part record (uncached memory) is in place before the count: no L2 write-back
+        // the part record's (agent-coherent) stores are acknowledged before the count: no L2
+        // write-back (a release would add buffer_wbl2 sc1)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         int last = 0;
         if (lane == 0) last = __hip_atomic_fetch_add(&sp->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nclaim - 1;
