@@ -22,6 +22,7 @@ EWK_ENOTEMPLATE = -2
 EWK_EHIP = -3
 EWK_ENOMEM = -4
 EWK_ENODEV = -5
+EWK_EOVERWRITTEN = -6
 EWK_EV_SKIPPED = 1
 EWK_EV_RESCORED = 2
 EWK_PUSH_DEVICE = 1
@@ -165,10 +166,17 @@ def load():
         return lib
 
 
+class RingOverwrittenError(ValueError):
+    """ewk_normalize_events: an event's samples were overwritten in its ring since its tick
+    (EWK_EOVERWRITTEN).  A ValueError, so callers that caught the old EWK_EINVAL still do."""
+
+
 def check(rc: int) -> None:
     if rc == EWK_OK:
         return
     msg = (load().ewk_last_error() or b"").decode(errors="replace")
+    if rc == EWK_EOVERWRITTEN:
+        raise RingOverwrittenError(msg)
     if rc in (EWK_EINVAL, EWK_ENOTEMPLATE):
         raise ValueError(msg)
     if rc == EWK_ENOMEM:

@@ -1022,7 +1022,7 @@ int ewk_normalize_events(ewk_engine* e, const ewk_event* events, int32_t n, doub
         if (nreq < 0) nreq += Rs;
         if (nreq == 0 && ev.length > 0) nreq = Rs;
         if (nreq + (e->tick - ev.tick) * blk > Rs)
-            return fail(EWK_EINVAL, "event " + std::to_string(i) + " (tick " + std::to_string(ev.tick) +
+            return fail(EWK_EOVERWRITTEN, "event " + std::to_string(i) + " (tick " + std::to_string(ev.tick) +
                                         "): the ring has overwritten its samples since (now tick " +
                                         std::to_string(e->tick) + "); read positives right after their poll");
     }

@@ -26,6 +26,8 @@ from typing import Callable, Optional
 
 import numpy as np
 
+from ._lib import RingOverwrittenError
+
 
 def shard_streams(n_streams: int, rank: int, world: int) -> tuple[int, int]:
     """(first stream, count) owned by `rank`: contiguous blocks, sizes differ by at most one."""
@@ -209,7 +211,7 @@ class PositiveCollector:
             self.pending.append(pos[len(take):])
         try:
             pcm = list(self.audio_fn(take))
-        except ValueError:
+        except RingOverwrittenError:
             # some events' samples were overwritten in their ring before this poll (a poll
             # more than (ring - request) / block ticks behind the cut: multi-tick pushes,
             # compact rings): those go on as records without PCM, the rest keep theirs
@@ -218,7 +220,7 @@ class PositiveCollector:
                 try:
                     pcm.extend(self.audio_fn(take[i:i + 1]))
                     keep.append(i)
-                except ValueError:
+                except RingOverwrittenError:   # (any other error is a bug: it propagates)
                     lost.append(i)
             if lost:
                 self.pending.append(take[lost])

@@ -29,7 +29,7 @@ extern "C" {
 #endif
 
 #define EWK_N_MFCC 20
-#define EWK_ABI_VERSION 3
+#define EWK_ABI_VERSION 4
 
 #define EWK_OK 0
 #define EWK_EINVAL (-1)       /* bad parameter            -> ValueError            */
@@ -37,6 +37,8 @@ extern "C" {
 #define EWK_EHIP (-3)         /* HIP runtime failure      -> RuntimeError          */
 #define EWK_ENOMEM (-4)       /* allocation failure       -> MemoryError           */
 #define EWK_ENODEV (-5)       /* no gfx950 device / bad device index -> RuntimeError */
+#define EWK_EOVERWRITTEN (-6) /* ewk_normalize_events: an event's samples were overwritten in its
+                                 ring since its tick -> RingOverwrittenError (a ValueError) */
 
 /* event flags */
 #define EWK_EV_SKIPPED 1      /* segment longer than max_segment_seconds: no level-2 call (wakeword.py:1113-1118) */

@@ -39,7 +39,7 @@ def test_defaults_are_reference_constants():
         (0.8, 0.3, 2.0, 0.4)
     assert (c.padding, c.max_segment_seconds, c.similarity_threshold) == (0.05, 3.0, 75.0)
     assert (c.min_threshold, c.initial_threshold, c.tick_seconds) == (0.005, 0.01, 0.1)
-    assert _lib.load().ewk_abi_version() == 3
+    assert _lib.load().ewk_abi_version() == 4
 
 
 def test_no_silent_cpu_fallback():

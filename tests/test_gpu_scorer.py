@@ -324,7 +324,8 @@ def test_every_segment_rescored_part_pool_overflow():
     ~24,000 8-frame chunks against the engine's 16,384 part records, so the slots listed after
     the pool runs out go serial (one wave each, claimed from their own list after every chunk
     is taken).  Every score must equal the fp64 API's (ewk_score_segments_f64, every slot
-    serial) within 1e-9, and every decision must follow it."""
+    serial) within 1e-9, and every decision must follow it; a sample spread over the batch
+    (pooled and serial slots alike) must equal the oracle's float64 path within 1e-9."""
     from easywakeword_amd import Engine
     segs = synth.ragged_segments(2024, 1500, 6400, 40000)
     e = Engine(rescore_margin=1e9)
@@ -338,6 +339,11 @@ def test_every_segment_rescored_part_pool_overflow():
         assert np.array_equal(np.isnan(sc), np.isnan(s64))
         assert float(np.max(np.abs(sc[ok] - s64[ok]))) <= 1e-9
         assert np.array_equal(mt.astype(bool)[ok], s64[ok] >= 75.0)
+        tm, ts = e.get_template()
+        for i in range(0, len(segs), 94):   # 16 segments over the listing order's whole range
+            cm, cs = mfcc_ref.extract_mfcc(np.asarray(segs[i], dtype=np.float64))
+            ref = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
+            assert score_close(sc[i], ref, 1e-9), (i, sc[i], ref)
     finally:
         e.close()
         f.close()
