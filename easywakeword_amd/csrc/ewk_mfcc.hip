@@ -1260,7 +1260,9 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
     }
     EWK_TS(tq4);
     EWK_TADD(5, tq3, tq4);
+#ifndef EWK_SKIP_EPI   // (timing experiment only: the statistics' finish and the score skipped)
     finish_stats(T, cref, s1, s2, lane, reinterpret_cast<double*>(scr));
+#endif
     EWK_TS(tq5);
     EWK_TADD(6, tq4, tq5);
 }
@@ -1720,7 +1722,11 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
             if (a.out_mean) a.out_mean[(int64_t)seg * NMFCC + lane] = cmf;
             if (a.out_std) a.out_std[(int64_t)seg * NMFCC + lane] = csf;
         }
+#ifndef EWK_SKIP_EPI
         if (a.has_template || a.list_all) score_epilogue<RING>(a, cmf, csf, tmf, tsf, lane, seg, v.len, theta_s);
+#else
+        if (lane == 0 && !RING) a.out_score[seg] = cmf + csf;
+#endif
         lds_order();
         EWK_TS(tw3);
         EWK_TADD(7, tw2, tw3);
