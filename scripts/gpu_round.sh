@@ -23,7 +23,7 @@ if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   R="${GRAFT_REPO_ROOT:-/root/repo}"
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 20 --warmup 10 --no-cpu-baseline --fixed-len 0 > "$R/gpurun_out/prof.log" 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -5 "$R/gpurun_out/prof.log"
-  python "$R/scripts/prof_summary.py" "$R/gpurun_out/prof" 10 > "$R/gpurun_out/kernel_stats.txt" 2>&1
+  python "$R/scripts/prof_summary.py" "$R/gpurun_out/prof" 10 20 > "$R/gpurun_out/kernel_stats.txt" 2>&1
   rm -f "$R/gpurun_out/prof/run_kernel_trace.csv"   # large; the stats csv and the summary stay
 fi
 if [ "$MODE" = all ] || [ "$MODE" = pmc ]; then

@@ -16,6 +16,7 @@ def short(name, n=70):
 
 def main():
     d, warm = sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 0   # > 0: only the bench's timed launches
     stats = list(csv.DictReader(open(os.path.join(d, "run_kernel_stats.csv"))))
     print(f"rocprofv3 --kernel-trace --stats: {d}")
     print(f"{'kernel':72s} {'calls':>6s} {'total ms':>10s} {'avg us':>10s} {'pct':>6s}")
@@ -28,7 +29,9 @@ def main():
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in tr if int(r["Grid_Size_X"]) == full]
     print(f"\nk_score_f32<0> bench-shaped dispatches (grid {full}): " + ", ".join(f"{x:.3f}" for x in durs) + " ms")
     if len(durs) > warm:
-        t = durs[warm:]
+        # (the launches after the timed ones -- short_length / fixed_length legs on the same grid --
+        # are left out when `steps` is given)
+        t = durs[warm:warm + steps] if steps else durs[warm:]
         print(f"mean after {warm} warmup launch(es): {sum(t) / len(t):.3f} ms over {len(t)} launches")
 
 
