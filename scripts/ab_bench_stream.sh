@@ -11,7 +11,7 @@ for r in $(seq 1 $R); do
       python -c "
 import json,sys; d=json.loads(sys.stdin.read()); s=d['streaming']
 line='8192: %.4f ms/tick (gate %.4f, scorer %.4f, rescore %.4f)' % (s['ms_per_tick'], s['gate_kernel_ms_per_tick'], s['scorer_kernel_ms_per_tick'], s['rescore_kernel_ms_per_tick'])
-b=d.get('streaming_100k')
+b=d.get('streaming_f32_max') or d.get('streaming_100k')
 if b: line += '; %d: %.4f ms/tick (gate %.4f)' % (b['streams'], b['ms_per_tick'], b['gate_kernel_ms_per_tick'])
 m=d.get('streaming_max')
 if m: line += '; %d: %.3f ms/tick (gate %.3f)' % (m['streams'], m['ms_per_tick'], m['gate_kernel_ms_per_tick'])

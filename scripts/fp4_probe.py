@@ -23,7 +23,7 @@ SRC = os.path.join(ROOT, "scripts", "probes", "fp4_probe.hip")
 
 
 def build():
-    for extra, out in (([], PROBE), (["-DFP4_TIMING"], PROBE + "_t")):
+    for extra, out in (([], PROBE), (["-DFP4_TIMING"], PROBE + "_t"), (["-DFP4_NW=4"], PROBE + "_nw4")):
         cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize", SRC,
                os.path.join(ROOT, "easywakeword_amd", "csrc", "ewk_tables.cpp"), "-o", out] + extra
         subprocess.run(cmd, check=True)
@@ -152,6 +152,12 @@ def mfcc_check():
     return 1 if nd else 0
 
 
+def occupancy():
+    """The pass at one wave per SIMD (4 waves per CU) against two (8 per CU), same grid."""
+    for exe in (PROBE + "_nw4", PROBE):
+        subprocess.run([exe, "time", "65536", "16000", "10"], check=True)
+
+
 def time_(quick=False):
     for L, n in ((16000, 65536),) if quick else ((16000, 65536), (6400, 65536), (32000, 32768)):
         subprocess.run([PROBE, "time", str(n), str(L), "10"], check=True)
@@ -169,5 +175,7 @@ if __name__ == "__main__":
         sys.exit(mfcc_check())
     elif what == "det":
         sys.exit(determinism())
+    elif what == "occ":
+        occupancy()
     else:
         time_(what == "quick")

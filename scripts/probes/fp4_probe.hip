@@ -18,14 +18,19 @@
 
 using namespace ewk;
 
-constexpr int NW = 8;
+#ifndef FP4_NW
+#define FP4_NW 8
+#endif
+constexpr int NW = FP4_NW;   // waves per workgroup (one workgroup per CU: 8 = two waves per SIMD)
 #ifdef FP4_TIMING
 __device__ unsigned long long g_tdbg[8];
 #define TARG , tdbg
 #else
 #define TARG
 #endif
-constexpr int PROBE_LDS = fp4::TABLE_BYTES + NW * fp4::STAGE_BYTES;
+// (padded past half the CU's LDS: one workgroup per CU whatever NW is)
+constexpr int PROBE_LDS_MIN = fp4::TABLE_BYTES + NW * fp4::STAGE_BYTES;
+constexpr int PROBE_LDS = PROBE_LDS_MIN > 82 * 1024 ? PROBE_LDS_MIN : 82 * 1024;
 
 template <int MODE>   // 0 check (write log-mel), 1 time (checksum), 2 time with DCT, 3 check MFCC (pass + DCT)
 __global__ __launch_bounds__(64 * NW, 1) void k_probe(const Tables* __restrict__ tab, const float* __restrict__ pcm,
