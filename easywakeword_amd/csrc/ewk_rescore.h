@@ -39,14 +39,19 @@ __device__ unsigned long long g_rs_dbg[16];
 #define EWK_RS_ADD(k, v) (void)atomicAdd(&g_rs_dbg[k], (unsigned long long)(v))
 // chunk sub-phases (s_memtime cycles summed over chunks): 0 samples + window, 1 FFT stages,
 // 2 untangle + power, 3 mel + log10, 4 DCT, 5 sums + flags, 6 chunks, 7 frame groups
+// (summed in registers, flushed once per chunk: an atomic inside the frame loop would put a
+// memory round trip into the next sample wait)
 __device__ unsigned long long g_rs_ph[8];
 #define EWK_RS_TS(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#define EWK_RS_PH(k, a, b) \
-    do { if (lane == 0) (void)atomicAdd(&g_rs_ph[k], (unsigned long long)((b) - (a))); } while (0)
+#define EWK_RS_PH(k, a, b) (rph[k] += (b) - (a))
+#define EWK_RS_PARAM , unsigned long long(&rph)[8]
+#define EWK_RS_ARG , rph
 #else
 #define EWK_RS_ADD(k, v) ((void)0)
 #define EWK_RS_TS(v)
 #define EWK_RS_PH(k, a, b) ((void)0)
+#define EWK_RS_PARAM
+#define EWK_RS_ARG
 #endif
 
 constexpr double kRsWindow = 1e-3;   // dB; the float32 max is within ~1e-5 dB of the fp64 one
@@ -266,7 +271,8 @@ __device__ __forceinline__ int rs_swz(int i) { return i ^ (((i >> 4) * 5) & 15);
 template <int NF>
 __device__ __forceinline__ void rs_frames(const double2 (&xw)[NF][4], const bool (&valid)[NF], const RsLane& c,
                                           unsigned char* wbuf, const unsigned char* smem, int lane, int f0,
-                                          double theta_s, double W, double& mx, bool& amb, bool& nanf, bool& clp) {
+                                          double theta_s, double W, double& mx, bool& amb, bool& nanf,
+                                          bool& clp EWK_RS_PARAM) {
     EWK_RS_TS(p0);
     double2 x[NF][4];
 #pragma unroll
@@ -471,6 +477,9 @@ __device__ void rs_chunk(const RsSrc<RING>& v, int T, int c, double theta_s, dou
     n = min(kRsFrames, T - t0);
     double m = -INFINITY;
     bool amb = false, nanf = false, clp = false;
+#ifdef EWK_RS_TIMING
+    unsigned long long rph[8] = {};
+#endif
     float smp[RS_NF][8];
 #pragma unroll
     for (int j = 0; j < RS_NF; ++j) rs_load(v, t0 + j, lane, smp[j]);   // (past T: range-checked zeros)
@@ -497,7 +506,7 @@ __device__ void rs_chunk(const RsSrc<RING>& v, int T, int c, double theta_s, dou
 #pragma unroll
             for (int j = 0; j < RS_NF; ++j) rs_load(v, t0 + f + RS_NF + j, lane, smp[j]);
         }
-        rs_frames<RS_NF>(xw, valid, cl, wbuf, smem, lane, f, theta_s, W, m, amb, nanf, clp);
+        rs_frames<RS_NF>(xw, valid, cl, wbuf, smem, lane, f, theta_s, W, m, amb, nanf, clp EWK_RS_ARG);
     }
     double A[8], B[8];
     EWK_RS_TS(d0);
@@ -523,6 +532,10 @@ __device__ void rs_chunk(const RsSrc<RING>& v, int T, int c, double theta_s, dou
     EWK_RS_TS(d2);
     EWK_RS_PH(5, d1, d2);
     EWK_RS_PH(6, 0ull, 1ull);
+#ifdef EWK_RS_TIMING
+    if (lane == 0)
+        for (int k = 0; k < 8; ++k) (void)atomicAdd(&g_rs_ph[k], rph[k]);
+#endif
 }
 
 // A part record's fields cross waves (any XCD) inside one launch: they are stored and loaded as
