@@ -202,7 +202,7 @@ __device__ double pw_sumsq(const MakeSrc& make, int n, const PwTree* full, const
     double acc = 0.0;
     for (int c0 = 0; c0 < n; c0 += kPwChunk) {
         const int cn = min(kPwChunk, n - c0);
-        acc += tree_sumsq(make(c0), cn == full->n ? full : rem, lane, val);
+        acc += tree_sumsq(make(c0), cn == kPwChunk ? full : rem, lane, val);   // (full->n == kPwChunk)
     }
     return acc;
 }
@@ -392,9 +392,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
     // stream's first tick is requested (LDS-DMA) as soon as this stream's last tick has
     // issued its stage reads, so its HBM latency overlaps this stream's FSM and stores
     int s = blockIdx.x * 4 + wave;
-    if (s >= g.n_streams) return;
     const int wstride = (int)gridDim.x * 4;
     const size_t per_wave = (size_t)g.val_len * 8 + (size_t)g.stage * 4;
+    // The trees of the block and last-window sums (lengths < one 8192 chunk) in LDS: every tree
+    // level reads its node indices, and from L1/L2 those dependent loads set the block sum's
+    // time (~4 us of a ~14 us stream-tick).  (The full-chunk trees, for callbacks > 8192
+    // samples, stay in global memory.)
+    PwTree* ltree = reinterpret_cast<PwTree*>(smem + 4 * per_wave);
+    {
+        static_assert(sizeof(PwTree) % 16 == 0, "trees are copied in 16-B pieces");
+        constexpr int kPieces = (int)(sizeof(PwTree) / 16);
+        const uint4* src0 = reinterpret_cast<const uint4*>(trees + kTreeBlockRem);
+        const uint4* src1 = reinterpret_cast<const uint4*>(trees + kTreeLastRem);
+        uint4* dst = reinterpret_cast<uint4*>(ltree);
+        for (int i = threadIdx.x; i < 2 * kPieces; i += blockDim.x) dst[i] = i < kPieces ? src0[i] : src1[i - kPieces];
+        __syncthreads();
+    }
+    if (s >= g.n_streams) return;
     unsigned char* w = smem + wave * per_wave;
     double* val = reinterpret_cast<double*>(w);
     float* stage = reinterpret_cast<float*>(w + (size_t)g.val_len * 8);
@@ -458,9 +472,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
     double* grms = g.block_rms + (int64_t)s * nb;
     double* sorted2 = g.sorted_rms + (int64_t)s * 2 * nb;
     const PwTree* tbf = trees + kTreeBlockFull;
-    const PwTree* tbr = trees + kTreeBlockRem;
+    const PwTree* tbr = ltree;
     const PwTree* tlf = trees + kTreeLastFull;
-    const PwTree* tlr = trees + kTreeLastRem;
+    const PwTree* tlr = ltree + 1;
     constexpr int RBn = RB > 0 ? RB : 1;
     double gr[RBn], srt[RBn];
     uint32_t dirty = 0;   // register path: bit j = gr[j] changed, bit RB + j = srt[j] changed (stored back only then)
@@ -830,7 +844,7 @@ hipError_t launch_gate(const GateArgs& g, hipStream_t s) {
     // one wave per stream (the hardware refills freed slots), up to kGateGridMax workgroups
     const int grid = std::min((g.n_streams + 3) / 4, kGateGridMax);
     const size_t per_wave = (size_t)g.val_len * 8 + (size_t)g.stage * 4;
-    const size_t lds = 4 * per_wave;
+    const size_t lds = 4 * per_wave + 2 * sizeof(PwTree);   // + the two sub-chunk trees (k_gate_ticks)
     const int64_t nl = std::min<int64_t>(g.n_last, g.ring_len);
     const bool dma = g.pcm16 == nullptr && g.stage >= g.block && g.stage >= nl;
     // 16-B pieces: every tick row 16-B aligned, whole 4-sample groups that never straddle the ring wrap
