@@ -43,7 +43,7 @@ struct PwTree {
     int32_t n;
     int32_t n_leaves;
     int32_t n_levels;
-    int32_t pad;
+    int32_t balanced;   // 1: 2^d <= 16 leaves of one length >= 8, combined pairwise in leaf order (tree_sumsq's register path)
     int16_t leaf_start[kPwMaxLeaves];
     int16_t leaf_len[kPwMaxLeaves];
     int16_t left[kPwMaxLeaves];     // internal node k = val[left[k]] + val[right[k]]

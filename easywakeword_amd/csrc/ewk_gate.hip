@@ -84,6 +84,19 @@ void build_pw_tree(int n, PwTree* t) {
         levels = nd.h;
     }
     t->n_levels = levels;
+    // balanced: every level pairs the previous level's nodes in order (node 2k with 2k + 1),
+    // there are 2^d <= 16 leaves and each has >= 8 elements (1,600: 16 leaves of 96 / 104)
+    bool bal = nleaf >= 1 && nleaf <= 16 && (nleaf & (nleaf - 1)) == 0;
+    for (int l = 0; bal && l < nleaf; ++l) bal = t->leaf_len[l] >= 8;
+    int first = 0, cnt = nleaf, k = 0;   // level h's nodes: ids [first, first + cnt)
+    for (int h = 0; bal && h < levels; ++h) {
+        for (int q = 0; bal && q < cnt / 2; ++q, ++k)
+            bal = t->left[k] == first + 2 * q && t->right[k] == first + 2 * q + 1 && k < t->level_end[h];
+        bal = bal && k == t->level_end[h];
+        first = h == 0 ? nleaf : first + cnt;
+        cnt /= 2;
+    }
+    t->balanced = bal && cnt == 1;
 }
 
 int gate_stage_len(int block, int64_t n_last) {
@@ -147,6 +160,63 @@ __device__ __forceinline__ double leaf_sumsq(const Src& src, int s, int n) {
     return res;
 }
 
+// DPP / permlane helpers for doubles (wave-uniform control)
+template <int CTRL, int BANKS>
+__device__ __forceinline__ double dpp_mov_d(double x) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), CTRL, 0xf, BANKS, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), CTRL, 0xf, BANKS, false);
+    return __hiloint2double(hi, lo);
+}
+// the value of lane ^ 16 (rows 0 <-> 1, 2 <-> 3) / lane ^ 32 (rows 0, 1 <-> 2, 3)
+template <int W>
+__device__ __forceinline__ double swap_rows_d(double x, int lane) {
+    const uint32_t lo = (uint32_t)__double2loint(x), hi = (uint32_t)__double2hiint(x);
+    const auto rl = W == 16 ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false)
+                            : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto rh = W == 16 ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false)
+                            : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    // (vdst, vsrc) = (x, x): the upper half of each pair finds the partner in vdst, the lower in vsrc
+    const bool upper = (lane & W) != 0;
+    return __hiloint2double((int)(upper ? rh[0] : rh[1]), (int)(upper ? rl[0] : rl[1]));
+}
+
+// A balanced chunk (build_pw_tree: 2^d <= 16 leaves of >= 8 elements, paired in order) without LDS:
+// lane = leaf % 8 * 8 + j runs accumulator j of leaf (leaf % 8) + 8 s for s = 0, 1 (numpy's
+// r[j] += x[i + j]^2, i = 8, 16, ...); the eight accumulators combine as
+// ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) by DPP exchanges (lane ^ 1, ^ 2, 7 - lane
+// within eight: every lane of the eight then holds the same bits, a + b == b + a), the tail
+// elements are added in order, and the leaves pair in order across lane groups (row_ror:8,
+// rows ^ 1, rows ^ 2, then set 0 + set 1) -- numpy's additions, operand for operand.
+template <typename Src>
+__device__ double tree_sumsq_bal(const Src& src, const PwTree* t, int lane) {
+    const int L = t->n_leaves;
+    const int j = lane & 7, li = lane >> 3;
+    double tot[2] = {0.0, 0.0};
+#pragma unroll
+    for (int set = 0; set < 2; ++set) {
+        if (8 * set >= L) break;   // (wave-uniform)
+        const int l = li + 8 * set < L ? li + 8 * set : 0;   // (lanes past the last leaf: a copy of leaf 0, unused)
+        const int s0 = t->leaf_start[l], m = t->leaf_len[l], m8 = m - m % 8;
+        double r;
+        { const double x = src(s0 + j); r = x * x; }
+        for (int i = 8; i < m8; i += 8) { const double x = src(s0 + i + j); r += x * x; }
+        r = r + dpp_mov_d<0xB1, 0xf>(r);   // quad_perm [1,0,3,2]: lane ^ 1
+        r = r + dpp_mov_d<0x4E, 0xf>(r);   // quad_perm [2,3,0,1]: lane ^ 2
+        r = r + dpp_mov_d<0x141, 0xf>(r);  // row_half_mirror: 7 - lane within eight
+        for (int i = m8; i < m; ++i) { const double x = src(s0 + i); r += x * x; }
+        // leaves of this set: pairs (row_ror:8), then rows ^ 1, rows ^ 2
+        if (L > 1) r = r + dpp_mov_d<0x128, 0xf>(r);   // row_ror:8
+        if (L > 2) r = r + swap_rows_d<16>(r, lane);
+        if (L > 4) r = r + swap_rows_d<32>(r, lane);
+        tot[set] = r;
+    }
+    // lane 0 holds its set's sum (for fewer than 8 leaves the rows past them hold copies of leaf
+    // 0); for 16 leaves the root adds the two halves in order.  Broadcast: a uniform result.
+    const double res = L > 8 ? tot[0] + tot[1] : tot[0];
+    return __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(res)),
+                            __builtin_amdgcn_readfirstlane(__double2loint(res)));
+}
+
 // One chunk (n = t->n elements of src) in numpy's pairwise order, wave-parallel.
 // val: per-wave LDS scratch of 10 * n_leaves doubles (node values, then the leaves'
 // 8 accumulators).  Each accumulator chain of a leaf runs on its own lane (numpy's
@@ -155,6 +225,7 @@ __device__ __forceinline__ double leaf_sumsq(const Src& src, int s, int n) {
 // Uniform result.
 template <typename Src>
 __device__ double tree_sumsq(const Src& src, const PwTree* t, int lane, double* val) {
+    if (t->balanced) return tree_sumsq_bal(src, t, lane);   // (the default 1,600-sample block: 16 leaves)
     const int L = t->n_leaves;
     double* acc8 = val + 2 * L;
     for (int q = lane; q < 8 * L; q += 64) {
