@@ -330,7 +330,10 @@ __device__ __forceinline__ double percentile25_sorted(const double* sorted, int 
 }
 
 // the register allocator must allow 4 waves per SIMD (121 VGPRs; 5 spill and run 37 % slower)
-constexpr int kGateWavesPerEU = 4;
+#ifndef EWK_GATE_WPE
+#define EWK_GATE_WPE 4
+#endif
+constexpr int kGateWavesPerEU = EWK_GATE_WPE;
 // workgroups of 4 waves, one stream per wave up to 524,288 streams, more loop inside the waves.
 // (Round 1 capped the grid at one resident wave per slot, 1,024 workgroups, so each wave ran
 // its streams in sequence behind the previous stream's final stores; letting the hardware
