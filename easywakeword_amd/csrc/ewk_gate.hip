@@ -99,6 +99,11 @@ void build_pw_tree(int n, PwTree* t) {
     t->balanced = bal && cnt == 1;
 }
 
+// per-wave LDS bytes of k_gate_ticks: tree values / sort scratch, then the stage (16-B aligned)
+__host__ __device__ inline size_t gate_wave_lds(int32_t val_len, int32_t stage, int stage_es) {
+    return (((size_t)val_len * 8 + 15) & ~(size_t)15) + (((size_t)stage * stage_es + 15) & ~(size_t)15);
+}
+
 int gate_stage_len(int block, int64_t n_last) {
     const int64_t m = std::max<int64_t>(block, n_last);
     if (m > 4096) return 0;              // long callbacks: sum straight from the ring
@@ -106,6 +111,13 @@ int gate_stage_len(int block, int64_t n_last) {
 }
 
 // ---- device ---------------------------------------------------------------------
+// The lane index through an empty asm: values derived from it (per-lane offsets) are then
+// computed where they are used instead of being hoisted out of the stream loop and kept live
+// (or spilled) across everything in between.
+__device__ __forceinline__ int lane_here(int lane) {
+    asm volatile("" : "+v"(lane));
+    return lane;
+}
 __device__ __forceinline__ void wave_sync() {
     asm volatile("" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -124,6 +136,13 @@ __device__ __forceinline__ void nt_store4(float* p, float4 v) {
 struct LdsSrc {
     const float* p;
     __device__ __forceinline__ float operator()(int i) const { return p[i]; }
+};
+
+// the int16 stage of the vector int16 path (DMA 3): the PCM16 value / 32768, exactly the float
+// the float stage held (half the LDS: five workgroups of four waves fit a CU)
+struct LdsSrc16 {
+    const int16_t* p;
+    __device__ __forceinline__ float operator()(int i) const { return (float)p[i] * (1.0f / 32768.0f); }
 };
 
 struct RingSrc {
@@ -465,9 +484,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
     // persistent over streams: wave w takes streams w, w + waves-in-grid, ...; the next
     // stream's first tick is requested (LDS-DMA) as soon as this stream's last tick has
     // issued its stage reads, so its HBM latency overlaps this stream's FSM and stores
-    int s = blockIdx.x * 4 + wave;
+    // (readfirstlane: the compiler then knows the stream, hence its state, is wave-uniform --
+    // scalar loads into SGPRs instead of a copy of GateStream in every lane's VGPRs)
+    int s = __builtin_amdgcn_readfirstlane((int)blockIdx.x * 4 + wave);
     const int wstride = (int)gridDim.x * 4;
-    const size_t per_wave = (size_t)g.val_len * 8 + (size_t)g.stage * 4;
+    constexpr int kStageEs = DMA == 3 ? 2 : 4;   // int16 stage for the vector int16 path
+    const size_t per_wave = gate_wave_lds(g.val_len, g.stage, kStageEs);
     // The trees of the block and last-window sums (lengths < one 8192 chunk) in LDS: every tree
     // level reads its node indices, and from L1/L2 those dependent loads set the block sum's
     // time (~4 us of a ~14 us stream-tick).  (The full-chunk trees, for callbacks > 8192
@@ -485,7 +507,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
     if (s >= g.n_streams) return;
     unsigned char* w = smem + wave * per_wave;
     double* val = reinterpret_cast<double*>(w);
-    float* stage = reinterpret_cast<float*>(w + (size_t)g.val_len * 8);
+    float* stage = reinterpret_cast<float*>(w + (((size_t)g.val_len * 8 + 15) & ~(size_t)15));
+    int16_t* stage16 = reinterpret_cast<int16_t*>(stage);   // (DMA 3)
+    // the staged samples [c0, ...) as a summation source
+    auto stage_src = [&](int c0) {
+        if constexpr (DMA == 3) return LdsSrc16{stage16 + c0};
+        else return LdsSrc{stage + c0};
+    };
 
     const int R = (int)g.ring_len;        // the reference ring: block grid, pointer, fill level
     const int Rs = (int)g.sring_len;      // samples stored per stream (== R unless compact)
@@ -509,9 +537,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
     u32x4 raw[kPcm16Pieces];
     auto load_vec = [&](int ss, int t) {
         const int16_t* src = g.pcm16 + (int64_t)ss * g.stride + (int64_t)t * g.tick_stride;
+        const int ln = lane_here(lane);
 #pragma unroll
         for (int c = 0; c < kPcm16Pieces; ++c) {
-            const int i0 = 8 * (lane + 64 * c);
+            const int i0 = 8 * (ln + 64 * c);
             raw[c] = i0 < fs ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + i0)) : u32x4{0, 0, 0, 0};
         }
     };
@@ -620,9 +649,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
             }
         }
         if (DMA == 3) {   // int16 pieces: ring (int16 as delivered, or widened) and stage stores
+            const int ln = lane_here(lane);
 #pragma unroll
             for (int c = 0; c < kPcm16Pieces; ++c) {
-                const int i0 = 8 * (lane + 64 * c);
+                const int i0 = 8 * (ln + 64 * c);
                 if (i0 < fs) {
                     int k = sp0 + i0;   // 8-sample groups never straddle the wrap (Rs % 8 == 0)
                     if (k >= Rs) k -= Rs;
@@ -639,10 +669,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
                         nt_store4(ring + k, make_float4(v[0], v[1], v[2], v[3]));
                         nt_store4(ring + k + 4, make_float4(v[4], v[5], v[6], v[7]));
                     }
-                    if (staged) {
-                        *reinterpret_cast<float4*>(stage + i0) = make_float4(v[0], v[1], v[2], v[3]);
-                        *reinterpret_cast<float4*>(stage + i0 + 4) = make_float4(v[4], v[5], v[6], v[7]);
-                    }
+                    if (staged) *reinterpret_cast<u32x4*>(stage16 + i0) = w;   // the int16 samples as delivered
                 }
             }
             if (t + 1 < g.n_ticks) load_vec(s, t + 1);   // next tick's samples, in flight during this tick
@@ -677,7 +704,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
             auto block_sum = [&](int b) -> double {
                 const int a0 = b * fs;
                 if (staged && a0 == p0)   // the block is exactly this tick's samples
-                    return pw_sumsq([&](int c0) { return LdsSrc{stage + c0}; }, fs, tbf, tbr, lane, val);
+                    return pw_sumsq(stage_src, fs, tbf, tbr, lane, val);
                 // reference-ring position a0 + c0 lives at sample-ring position sp0 + (a0 + c0 - p0)
                 // (the identity for the full ring; compact rings only reach this path for
                 // blocks written within the last Rs samples)
@@ -764,7 +791,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
             // filling a compact ring: keep this block's RMS now (its samples will not all
             // be in the sample ring when the reference ring first fills)
             const int b = p0 / fs;
-            const double v = sqrt(pw_sumsq([&](int c0) { return LdsSrc{stage + c0}; }, fs, tbf, tbr, lane, val) /
+            const double v = sqrt(pw_sumsq(stage_src, fs, tbf, tbr, lane, val) /
                                   (double)fs);
             if (RB > 0) reg_set(gr, b, v, lane, dirty);
             else if (lane == 0) grms[b] = v;
@@ -776,8 +803,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kGateWavesP
             if (have_reuse) {
                 sum = reuse_sum;
             } else if (staged && nl <= fs) {   // the window lies in this tick's samples
-                const float* base = stage + (fs - nl);
-                sum = pw_sumsq([&](int c0) { return LdsSrc{base + c0}; }, nl, tlf, tlr, lane, val);
+                sum = pw_sumsq([&](int c0) { return stage_src(fs - nl + c0); }, nl, tlf, tlr, lane, val);
             } else {
                 int first = st.spos - nl;
                 if (first < 0) first += Rs;
@@ -917,8 +943,7 @@ hipError_t launch_gate(const GateArgs& g, hipStream_t s) {
     if (g.n_streams <= 0 || g.n_ticks <= 0) return hipSuccess;
     // one wave per stream (the hardware refills freed slots), up to kGateGridMax workgroups
     const int grid = std::min((g.n_streams + 3) / 4, kGateGridMax);
-    const size_t per_wave = (size_t)g.val_len * 8 + (size_t)g.stage * 4;
-    const size_t lds = 4 * per_wave + 2 * sizeof(PwTree);   // + the two sub-chunk trees (k_gate_ticks)
+    // (the int16 vector path stages int16; every other path float)
     const int64_t nl = std::min<int64_t>(g.n_last, g.ring_len);
     const bool dma = g.pcm16 == nullptr && g.stage >= g.block && g.stage >= nl;
     // 16-B pieces: every tick row 16-B aligned, whole 4-sample groups that never straddle the ring wrap
@@ -929,6 +954,10 @@ hipError_t launch_gate(const GateArgs& g, hipStream_t s) {
     const bool vec16 = g.pcm16 != nullptr && g.block % 8 == 0 && g.block <= 512 * kPcm16Pieces &&
                        g.stride % 8 == 0 && g.tick_stride % 8 == 0 && g.sring_len % 8 == 0 &&
                        ((uintptr_t)g.pcm16 & 15) == 0;
+    // the DMA 3 instantiations (and only they) stage int16
+    const bool i16stage = vec16 && !dma4 && g.n_blocks <= 64 * kGateRegMax;
+    const size_t lds = 4 * gate_wave_lds(g.val_len, g.stage, i16stage ? 2 : 4) +
+                       2 * sizeof(PwTree);   // + the two sub-chunk trees (k_gate_ticks)
     if (g.n_blocks <= 128) {
         if (dma4) hipLaunchKernelGGL((k_gate_ticks<2, 2>), dim3(grid), dim3(256), lds, s, g);
         else if (vec16) hipLaunchKernelGGL((k_gate_ticks<2, 3>), dim3(grid), dim3(256), lds, s, g);
