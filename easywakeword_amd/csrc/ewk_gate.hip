@@ -358,7 +358,10 @@ constexpr int kGateWavesPerEU = EWK_GATE_WPE;
 // its streams in sequence behind the previous stream's final stores; letting the hardware
 // refill freed slots with new waves instead took the tick from 11.6 to 9.2 ms at 2 M streams,
 // 0.75 to 0.65 ms at 131,072 and 77 to 72 us at 8,192.)
-constexpr int kGateGridMax = 131072;
+#ifndef EWK_GATE_GRID_MAX
+#define EWK_GATE_GRID_MAX 131072
+#endif
+constexpr int kGateGridMax = EWK_GATE_GRID_MAX;
 constexpr int kDma4Chunks = 8;
 constexpr int kPcm16Pieces = 4;    // int16 path: ticks of up to 4 * 512 samples in 16-B pieces
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));     // 16-B DMA path: ticks of up to 8 * 256 samples copied to the ring in one batch
