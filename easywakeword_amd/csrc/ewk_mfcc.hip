@@ -46,6 +46,7 @@
 #include <math.h>
 
 #include "ewk_internal.h"
+#include "ewk_db64.h"   // (the fp64 re-score's 10 log10, ewk_rescore.h)
 
 // s_setprio 1 over the frame-pass LDS phases (window, transposes, mel): -0.4 %
 #define EWK_SETPRIO(v) __builtin_amdgcn_s_setprio(v)

@@ -358,9 +358,13 @@ __device__ __forceinline__ void rs_frames(const double2 (&xw)[NF][4], const bool
     for (int h = 0; h < 2; ++h) {
         const int m = h ? NMEL - 1 - lane : lane;
         const int lo = mlo[m], o0 = moff[m], nw = moff[m + 1] - o0;
+        // every weight read unconditionally (clamped index), then selected: a conditional read
+        // made each weight its own exec-masked block (24 branches per frame pair)
         float ww[kRsMelW];
 #pragma unroll
-        for (int q = 0; q < kRsMelW; ++q) ww[q] = q < nw ? mw[min(o0 + q, RS_MW_N - 1)] : 0.0f;
+        for (int q = 0; q < kRsMelW; ++q) ww[q] = mw[min(o0 + q, RS_MW_N - 1)];
+#pragma unroll
+        for (int q = 0; q < kRsMelW; ++q) ww[q] = q < nw ? ww[q] : 0.0f;
 #pragma unroll
         for (int j = 0; j < NF; ++j) {
             const double* P = reinterpret_cast<const double*>(wbuf + RS_BUF) + 512 * j;
@@ -377,7 +381,8 @@ __device__ __forceinline__ void rs_frames(const double2 (&xw)[NF][4], const bool
             acc = pw[0] + (double)ww[0] + (double)nw;
 #endif
 #ifndef EWK_RS_SKIP_LOG
-            const double db = 10.0 * log10(acc < 1e-10 ? 1e-10 : acc);   // np.maximum: NaN propagates
+            // (ewk_db64.h: 10 log10 in ~30 float64 instructions; the library's log10 takes ~100)
+            const double db = ewk_db64(acc < 1e-10 ? 1e-10 : acc);   // np.maximum: NaN propagates
 #else
             const double db = acc;
 #endif
@@ -385,12 +390,13 @@ __device__ __forceinline__ void rs_frames(const double2 (&xw)[NF][4], const bool
             // as with +0, and db is never -0.0 (10 log10(acc), acc >= 1e-10), so -0.0 also marks
             // the B operand for rs_dct (no second tile)
             xa[m * kRsFrames + f0 + j] = db >= theta_s ? db : -0.0;
-            if (valid[j]) {
-                clp = clp || !(db >= theta_s);
-                mx = fmax(mx, db);
-                amb = amb || fabs(db - theta_s) <= W;
-                nanf = nanf || db != db;
-            }
+            // selects, not a branch: the four bands' log10 chains (~90 dependent fp64 ops
+            // each) stay in one block, where the scheduler can interleave them
+            const bool vj = valid[j];
+            clp = clp | (vj & !(db >= theta_s));
+            mx = vj ? fmax(mx, db) : mx;
+            amb = amb | (vj & (fabs(db - theta_s) <= W));
+            nanf = nanf | (vj & (db != db));
         }
     }
     wave_sync();

@@ -11,7 +11,7 @@ for f in easywakeword_amd/csrc/ewk_gather.hip; do   # sources that older revisio
   if [ "$REV" = "WT" ] || git -C "$R" cat-file -e "$REV:$f" 2>/dev/null; then SRCS="$SRCS $(basename $f)"; fi
 done
 HDRS="ewk_internal.h ewk_gate.h"
-for h in ewk_rescore.h ewk_fp4.h ewk_fp4_mel.h; do   # headers that older revisions lack
+for h in ewk_rescore.h ewk_fp4.h ewk_fp4_mel.h ewk_db64.h; do   # headers that older revisions lack
   if [ "$REV" = "WT" ] || git -C "$R" cat-file -e "$REV:easywakeword_amd/csrc/$h" 2>/dev/null; then HDRS="$HDRS $h"; fi
 done
 for s in $SRCS $HDRS; do
