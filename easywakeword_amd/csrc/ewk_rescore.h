@@ -103,10 +103,10 @@ __device__ __forceinline__ RsArgs rs_args(const ScoreArgs& a) {
 #define EWK_RS_NW 8
 #endif
 constexpr int RS_NW = EWK_RS_NW;
-// LDS of the re-score launch.  The DCT table keeps bands 0..63 only: the DCT-II rows are
-// (anti)symmetric, D[k][127 - m] = (-1)^k D[k][m] (the fp64 table is built that way, exactly).
-constexpr int RS_D = 0;                                     // double [NMEL / 2][NMFCC]
-constexpr int RS_MLO = RS_D + (NMEL / 2) * NMFCC * 8;       // int [NMEL]
+// LDS of the re-score launch.  The DCT table is whole, [m][k]: the half table (the DCT-II rows
+// are (anti)symmetric) cost a mirrored index and a sign per band in the DCT's inner loop.
+constexpr int RS_D = 0;                                     // double [NMEL][NMFCC]
+constexpr int RS_MLO = RS_D + NMEL * NMFCC * 8;             // int [NMEL]
 constexpr int RS_MOFF = RS_MLO + NMEL * 4;                  // int [NMEL + 1]
 constexpr int RS_MW = RS_MOFF + (NMEL + 4) * 4;             // float [2 NBIN + 2 NMEL]
 constexpr int RS_MW_N = 2 * NBIN + 2 * NMEL;
@@ -196,7 +196,7 @@ __device__ void rs_load_tables(const Tables64* __restrict__ tb, unsigned char* s
     int* mlo = reinterpret_cast<int*>(smem + RS_MLO);
     int* moff = reinterpret_cast<int*>(smem + RS_MOFF);
     float* mw = reinterpret_cast<float*>(smem + RS_MW);
-    for (int i = threadIdx.x; i < (NMEL / 2) * NMFCC; i += blockDim.x) {
+    for (int i = threadIdx.x; i < NMEL * NMFCC; i += blockDim.x) {
         const int m = i / NMFCC, k = i % NMFCC;
         D[i] = tb->dct[k * NMEL + m];
     }
@@ -408,8 +408,11 @@ __device__ __forceinline__ void rs_frames(const double2 (&xw)[NF][4], const bool
 // DCT of the chunk's n frames split at theta_s: lane k < 20 returns A_k, B_k of frames 0..7
 // (A: the values x >= theta_s, B: the weights of the others -- NaN included -- which the
 // clamp replaces by theta; rs_frame stored those as -0.0).  Lanes (k, h) = (l % 20, l / 20),
-// l < 60, take bands [43 h, 43 h + 43), the next band's reads issued before this band's FMAs;
-// the thirds are added in a fixed order (h = 0, 1, 2).
+// l < 60, take bands [43 h, 43 h + 43), EWK_RS_DCT_U bands' reads in flight together; the
+// thirds are added in a fixed order (h = 0, 1, 2).
+#ifndef EWK_RS_DCT_U
+#define EWK_RS_DCT_U 2
+#endif
 __device__ __forceinline__ void rs_dct(const unsigned char* smem, unsigned char* wbuf, int lane, bool need_b,
                                        double (&A)[8], double (&B)[8]) {
     const double* D = reinterpret_cast<const double*>(smem + RS_D);
@@ -424,19 +427,11 @@ __device__ __forceinline__ void rs_dct(const unsigned char* smem, unsigned char*
 #else
         const int m1 = m0 + 1;
 #endif
-        // D[k][m] = (-1)^k D[k][127 - m]: the sign is applied at use, after the load's wait
-        auto draw = [&](int m) { return D[(m >= NMEL / 2 ? NMEL - 1 - m : m) * NMFCC + k]; };
-        double dn = draw(m0);
-        double4 n0 = reinterpret_cast<const double4*>(xa + m0 * kRsFrames)[0];
-        double4 n1 = reinterpret_cast<const double4*>(xa + m0 * kRsFrames)[1];
-        for (int m = m0; m < m1; ++m) {
-            const double d = m >= NMEL / 2 && (k & 1) ? -dn : dn;
+        const double* dp = D + k;
+        const double4* xp = reinterpret_cast<const double4*>(xa);
+        // one band: A[f] += D[k][m] x[m][f]; B[f] += D[k][m] where x[m][f] was clamped (-0.0)
+        auto band = [&](double d, const double4& n0, const double4& n1) {
             const double av[8] = {n0.x, n0.y, n0.z, n0.w, n1.x, n1.y, n1.z, n1.w};
-            if (m + 1 < m1) {
-                dn = draw(m + 1);
-                n0 = reinterpret_cast<const double4*>(xa + (m + 1) * kRsFrames)[0];
-                n1 = reinterpret_cast<const double4*>(xa + (m + 1) * kRsFrames)[1];
-            }
 #pragma unroll
             for (int f = 0; f < 8; ++f) A[f] = fma(d, av[f], A[f]);
             if (need_b) {   // (wave-uniform: a chunk with no clamped value has B = 0 exactly)
@@ -446,7 +441,24 @@ __device__ __forceinline__ void rs_dct(const unsigned char* smem, unsigned char*
                     B[f] = fma(d, clamped ? 1.0 : 0.0, B[f]);
                 }
             }
+        };
+        // kRsDctU bands per step, their reads issued together (one LDS wait per step, bands in
+        // order: the same sums as one band per step)
+        constexpr int kRsDctU = EWK_RS_DCT_U;
+        int m = m0;
+        for (; m + kRsDctU <= m1; m += kRsDctU) {
+            double d[kRsDctU];
+            double4 n[kRsDctU][2];
+#pragma unroll
+            for (int u = 0; u < kRsDctU; ++u) {
+                d[u] = dp[(m + u) * NMFCC];
+                n[u][0] = xp[2 * (m + u)];
+                n[u][1] = xp[2 * (m + u) + 1];
+            }
+#pragma unroll
+            for (int u = 0; u < kRsDctU; ++u) band(d[u], n[u][0], n[u][1]);
         }
+        for (; m < m1; ++m) band(dp[m * NMFCC], xp[2 * m], xp[2 * m + 1]);
     }
     wave_sync();
     if (lane >= NMFCC && lane < 60) {   // thirds 1, 2 park their sums in the (consumed) XA tile
