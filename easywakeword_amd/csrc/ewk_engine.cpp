@@ -431,9 +431,9 @@ int ewk_create(ewk_engine** out, int device, int32_t n_streams, const ewk_config
         Tables64* t64 = reinterpret_cast<Tables64*>(buf64.data());
         build_tables64(t64);
         for (int m = 0; m < NMEL; ++m)
-            if (t64->mel_off[m + 1] - t64->mel_off[m] > kRsMelW) {
+            if (t64->mel_off[m + 1] - t64->mel_off[m] > (m < NMEL / 2 ? kRsMelWLo : kRsMelW)) {
                 ewk_destroy(e);
-                return fail(EWK_EHIP, "mel filterbank band wider than the fp64 path's window (kRsMelW)");
+                return fail(EWK_EHIP, "mel filterbank band wider than the fp64 path's window (kRsMelWLo / kRsMelW)");
             }
         if ((err = hipMalloc(&e->d_tab64, sizeof(Tables64))) != hipSuccess) return bail(err, "tables64");
         if ((err = hipMemcpy(e->d_tab64, t64, sizeof(Tables64), hipMemcpyHostToDevice)) != hipSuccess)

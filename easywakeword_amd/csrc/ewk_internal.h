@@ -93,6 +93,7 @@ void build_tables64(Tables64* t);
 constexpr int kRsFrames = 8;   // frames per re-score chunk
 constexpr int kRsCtl = 8;      // ints of ScoreArgs::rs_ctl
 constexpr int kRsMelW = 12;    // widest Slaney band of the basis in bins (fp64 mel window; checked at engine creation)
+constexpr int kRsMelWLo = 3;   // widest of bands 0..63 (the fp64 path's window for a lane's low band; checked too)
 struct RsSlot {
     int32_t seg;       // segment (linear) or event (ring) index
     int32_t T;         // frames

@@ -351,18 +351,20 @@ __device__ __forceinline__ void rs_frames(const double2 (&xw)[NF][4], const bool
     const int* moff = reinterpret_cast<const int*>(smem + RS_MOFF);
     const float* mw = reinterpret_cast<const float*>(smem + RS_MW);
     double* xa = reinterpret_cast<double*>(wbuf + RS_XA);
-    // a fixed kRsMelW-wide window per band, read unconditionally (one LDS round trip, no
-    // branch); past the band's support the weight and the power are selected to 0, and
-    // fma(0, 0, acc) = acc, so the sum is the band's, in bin order
+    // a fixed-width window per band, read unconditionally (one LDS round trip, no branch):
+    // kRsMelWLo bins for the lane's low band (bands 0..63 span <= 3 bins), kRsMelW for its high
+    // one; past the band's support the weight is selected to 0, and fma(0, p, acc) = acc, so the
+    // sum is the band's, in bin order
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         const int m = h ? NMEL - 1 - lane : lane;
+        const int kw = h ? kRsMelW : kRsMelWLo;   // (h unrolled: a constant)
         const int lo = mlo[m], o0 = moff[m], nw = moff[m + 1] - o0;
         // every weight read unconditionally (clamped index), then selected: a conditional read
         // made each weight its own exec-masked block (24 branches per frame pair)
         float ww[kRsMelW];
 #pragma unroll
-        for (int q = 0; q < kRsMelW; ++q) ww[q] = mw[min(o0 + q, RS_MW_N - 1)];
+        for (int q = 0; q < kRsMelW; ++q) ww[q] = q < kw ? mw[min(o0 + q, RS_MW_N - 1)] : 0.0f;
 #pragma unroll
         for (int q = 0; q < kRsMelW; ++q) ww[q] = q < nw ? ww[q] : 0.0f;
 #pragma unroll
@@ -370,13 +372,14 @@ __device__ __forceinline__ void rs_frames(const double2 (&xw)[NF][4], const bool
             const double* P = reinterpret_cast<const double*>(wbuf + RS_BUF) + 512 * j;
             double pw[kRsMelW];
 #pragma unroll
-            for (int q = 0; q < kRsMelW; ++q) pw[q] = P[lo + q];   // lo + q < 2 * 256: inside the frame's buffer
+            for (int q = 0; q < kRsMelW; ++q) pw[q] = q < kw ? P[lo + q] : 0.0;   // lo + q < 2 * 256: inside the frame's buffer
             double acc = 0.0;
 #ifndef EWK_RS_SKIP_MEL
             // past the band: weight 0 times a finite power of this frame (its FFT buffer; a NaN
             // there means NaN samples, and then every bin is NaN) adds +-0, and acc + -0 = acc
 #pragma unroll
-            for (int q = 0; q < kRsMelW; ++q) acc = fma((double)ww[q], pw[q], acc);
+            for (int q = 0; q < kRsMelW; ++q)
+                if (q < kw) acc = fma((double)ww[q], pw[q], acc);
 #else   // (timing experiment: one bin per band)
             acc = pw[0] + (double)ww[0] + (double)nw;
 #endif
