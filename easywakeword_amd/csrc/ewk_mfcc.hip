@@ -1086,6 +1086,7 @@ __device__ __forceinline__ float scout_tiles(const SegSrc<RING>& v, int ntile, i
 // instead holds a reservation for a whole segment and costs more at the batch tail.)
 struct WorkAhead {
     int state = 0;      // 0 none, 1 index requested (lane 0), 2 index known, 3 described
+    bool first = true;  // the wave's first claim: its own index, no atomic
     int idx = 0;
     int seg = 0;
     int64_t start = 0;
@@ -1097,11 +1098,21 @@ struct WorkCtx {
     const ScoreArgs* a;
     int base, count;
     bool ahead;         // claim the next item during this segment
+    int wid, nw;        // this wave's index in the grid, the grid's waves
 };
 
+// The first item of every wave is its own index (work items 0 .. nw - 1), the rest come from
+// the counter: one device-scope fetch-add address serves ~1 claim per 11 ns, and a launch's
+// first claims all arrive together (2,048 of them: ~23 us for the last;
+// scripts/probes/atomic_probe.hip).
 template <int RING>
 __device__ __forceinline__ void work_claim(const WorkCtx& c, WorkAhead& w, int lane) {
-    if (lane == 0) w.idx = atomicAdd(c.a->work, 1);
+    if (w.first) {
+        w.idx = c.wid;
+        w.first = false;
+    } else if (lane == 0) {
+        w.idx = c.nw + atomicAdd(c.a->work, 1);
+    }
     w.state = 1;
 }
 template <int RING>
@@ -1687,7 +1698,7 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
 #ifdef EWK_TIMING
     uint64_t dbg[kDbgN] = {};
 #endif
-    const WorkCtx wc = {&a, base, count, true};
+    const WorkCtx wc = {&a, base, count, true, (int)blockIdx.x * WAVES + wave, (int)gridDim.x * WAVES};
     WorkAhead nx;
     for (;;) {
         EWK_TS(tw0);

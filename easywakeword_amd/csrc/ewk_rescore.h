@@ -749,11 +749,22 @@ struct RsClaim {
     int slot = -1, unit = 0, seg = 0, T = 0, base = 0, serial = 0, nclaim = 0;
     float theta_s = 0.0f;
 };
-__device__ __forceinline__ RsClaim rs_claim(const RsArgs& a, int n_parts, int n_serial) {
+// A wave's first claim of the launch is part record (its index in the grid) -- no atomic: one
+// device-scope fetch-add address serves ~1 claim per 11 ns and the launch's 2,048 waves would
+// all claim at once (~23 us for the last; scripts/probes/atomic_probe.hip) -- the rest come
+// from the cursor, offset by the grid's waves.
+__device__ __forceinline__ int rs_grid_waves() { return (int)gridDim.x * RS_NW; }
+__device__ __forceinline__ RsClaim rs_claim(const RsArgs& a, int n_parts, int n_serial, int& first) {
     RsClaim r;
     int s = -1;
     for (;;) {
-        const int g = __hip_atomic_fetch_add(&a.rs_ctl[4], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int g;
+        if (first >= 0) {
+            g = first;
+            first = -1;
+        } else {
+            g = rs_grid_waves() + __hip_atomic_fetch_add(&a.rs_ctl[4], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         EWK_RS_ADD(12, 1);
         if (g >= n_parts) break;
         s = a.rs_parts[g].slot;
@@ -784,8 +795,11 @@ __device__ __forceinline__ int rs_n_serial(const RsArgs& a) {
 }
 
 // One wave drains the list until nothing is claimable; true if it finished a slot.
+// first_claim: the launch's main drain (a wave's own part record first); the last workgroup's
+// second drain takes cursor claims only.
 template <int RING>
-__device__ __attribute__((noinline)) bool rs_drain(const RsArgs& a, unsigned char* smem, int wave, int lane) {
+__device__ __attribute__((noinline)) bool rs_drain(const RsArgs& a, unsigned char* smem, int wave, int lane,
+                                                   bool first_claim) {
     unsigned char* wbuf = smem + RS_WAVES + wave * RS_WAVE_BYTES;
     if (lane == 0) EWK_RS_ADD(0, 1);   // waves that drain
 #ifdef EWK_RS_TIMING
@@ -794,9 +808,10 @@ __device__ __attribute__((noinline)) bool rs_drain(const RsArgs& a, unsigned cha
     RsLane cl;
     bool have_lane = false, finished = false;
     const int n_parts = rs_n_parts(a), n_serial = rs_n_serial(a);
+    int first = first_claim ? (int)blockIdx.x * RS_NW + wave : -1;   // (lane 0's)
     for (;;) {
         RsClaim c;
-        if (lane == 0) c = rs_claim(a, n_parts, n_serial);
+        if (lane == 0) c = rs_claim(a, n_parts, n_serial, first);
         const int slot = __shfl(c.slot, 0, 64);
         if (slot < 0) break;
         const int unit = __shfl(c.unit, 0, 64), seg = __shfl(c.seg, 0, 64), T = __shfl(c.T, 0, 64);
@@ -859,8 +874,11 @@ __device__ __attribute__((noinline)) bool rs_drain(const RsArgs& a, unsigned cha
 }
 
 // Anything listed that no wave has taken yet (thread 0)?
-__device__ __forceinline__ bool rs_pending(const RsArgs& a) {
-    return __hip_atomic_load(&a.rs_ctl[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < rs_n_parts(a) ||
+// first_claim: this workgroup's waves have not drained yet (their own part records count).
+__device__ __forceinline__ bool rs_pending(const RsArgs& a, bool first_claim) {
+    const int n_parts = rs_n_parts(a);
+    return (first_claim && (int)blockIdx.x * RS_NW < n_parts) ||
+           rs_grid_waves() + __hip_atomic_load(&a.rs_ctl[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n_parts ||
            __hip_atomic_load(&a.rs_ctl[5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < rs_n_serial(a);
 }
 
@@ -933,14 +951,14 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem) {
         return;
     }
     bool loaded = false, finished = false;
-    if (threadIdx.x == 0) flag[1 + RS_NW] = rs_pending(ra);
+    if (threadIdx.x == 0) flag[1 + RS_NW] = rs_pending(ra, true);
     __syncthreads();
     if (flag[1 + RS_NW]) {
         if (threadIdx.x == 0) EWK_RS_ADD(9, 1);   // workgroups that drain
         rs_load_tables(a.tab64, smem);
         __syncthreads();
         loaded = true;
-        finished = rs_drain<RING>(ra, smem, wave, lane);
+        finished = rs_drain<RING>(ra, smem, wave, lane, true);
     }
     if (lane == 0) flag[1 + wave] = finished;
     __syncthreads();
@@ -958,14 +976,14 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem) {
 #endif
     __threadfence();   // acquire what every other workgroup released before its count
     // the last workgroup: every other has drained and counted out
-    if (threadIdx.x == 0) flag[1 + RS_NW] = rs_pending(ra);
+    if (threadIdx.x == 0) flag[1 + RS_NW] = rs_pending(ra, false);
     __syncthreads();
     if (flag[1 + RS_NW]) {
         if (!loaded) {
             rs_load_tables(a.tab64, smem);
             __syncthreads();
         }
-        rs_drain<RING>(ra, smem, wave, lane);
+        rs_drain<RING>(ra, smem, wave, lane, false);
     }
     __syncthreads();
     tick_end<RING>(a);
