@@ -25,6 +25,9 @@ EWK_ENODEV = -5
 EWK_EOVERWRITTEN = -6
 EWK_EV_SKIPPED = 1
 EWK_EV_RESCORED = 2
+# |MFCC mean vector| below which a segment's score comes from the fp64 re-score (the scorer's
+# kTinyMean, csrc/ewk_mfcc.hip; tests/test_rescore_criteria.py keeps the two equal)
+RESCORE_TINY_MEAN = 32.0
 EWK_PUSH_DEVICE = 1
 EWK_PCM_DEVICE = 1
 EWK_OUT_DEVICE = 4

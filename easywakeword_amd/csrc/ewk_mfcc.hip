@@ -79,6 +79,12 @@ namespace ewk {
 #ifdef EWK_TIMING
 __device__ unsigned long long g_ewk_dbg[kDbgN];
 #endif
+// Why segments go to the fp64 re-score (debug builds with -DEWK_LIST_STATS only,
+// scripts/list_reasons.py): [0] listed, [1..4] segments meeting each criterion (margin, short,
+// nearly stationary, vanishing mean; a segment can meet several), [5..9] their frames.
+#ifdef EWK_LIST_STATS
+__device__ unsigned long long g_ewk_list[10];
+#endif
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
@@ -141,7 +147,13 @@ constexpr int W_BYTES = W_SPEC + (kSpecOrder + kSpecTiles) * 4;
 constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
 constexpr int LDS_BYTES = L_WG + 16 + 8 * WAVES;
 constexpr int kRescoreFrames = 16;
-constexpr double kTinyMean = 64.0;  // |mean vector| below which the fp64 path decides
+// |mean vector| below which the fp64 path decides (round 5: 32, was 64 -- the float32 score error
+// scales as ~2.8e-3 / |mean| on streaming events, <= 1.2e-5 observed above 32: DESIGN.md
+// numerics, profiles/r05_v26_mean_err.txt; easywakeword_amd/_lib.py RESCORE_TINY_MEAN mirrors it)
+#ifndef EWK_TINY_MEAN
+#define EWK_TINY_MEAN 32.0
+#endif
+constexpr double kTinyMean = EWK_TINY_MEAN;
                                     // (loud audio, c0 cancelling: DESIGN.md numerics)
 constexpr double kTinyStd = 20.0;   // |std vector| below which the fp64 path decides (bench batch >= 24.8,
                                     // streaming events >= 32.5: scripts/std_norm_dist.py)
@@ -1550,6 +1562,17 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, fl
             // is a rounding artefact).
             near = near || fabs(score - a.threshold) < a.rescore_margin || (1 + len / HOP) <= kRescoreFrames ||
                    (std2 > 0.0 && std2 < kTinyStd * kTinyStd) || mean2 < kTinyMean * kTinyMean;
+#ifdef EWK_LIST_STATS
+            if (near) {
+                const unsigned long long T = 1 + len / HOP;
+                const bool why[4] = {fabs(score - a.threshold) < a.rescore_margin, (int)T <= kRescoreFrames,
+                                     std2 > 0.0 && std2 < kTinyStd * kTinyStd, mean2 < kTinyMean * kTinyMean};
+                atomicAdd(&g_ewk_list[0], 1ull);
+                atomicAdd(&g_ewk_list[5], T);
+                for (int k = 0; k < 4; ++k)
+                    if (why[k]) { atomicAdd(&g_ewk_list[1 + k], 1ull); atomicAdd(&g_ewk_list[6 + k], T); }
+            }
+#endif
             if (RING) {
                 a.events[seg].score = score;
                 a.events[seg].match = match;
@@ -1766,6 +1789,17 @@ extern "C" int ewk_debug_rs_ph(unsigned long long* out) {   // chunk sub-phase c
     unsigned long long z[8] = {};
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ewk::g_rs_ph), sizeof(z)) != hipSuccess) return -3;
     if (hipMemcpyToSymbol(HIP_SYMBOL(ewk::g_rs_ph), z, sizeof(z)) != hipSuccess) return -3;
+    return 0;
+}
+namespace ewk {
+#endif
+
+#ifdef EWK_LIST_STATS
+}  // namespace ewk
+extern "C" int ewk_debug_list(unsigned long long* out) {   // read and reset (debug builds only)
+    unsigned long long z[10] = {};
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ewk::g_ewk_list), sizeof(z)) != hipSuccess) return -3;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(ewk::g_ewk_list), z, sizeof(z)) != hipSuccess) return -3;
     return 0;
 }
 namespace ewk {
