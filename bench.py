@@ -661,21 +661,21 @@ def streaming_host_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, ri
     stage = [torch.empty(per, dtype=host.dtype, device=dev) for _ in range(2)]
     cs = torch.cuda.Stream(dev)
     es_ = torch.cuda.ExternalStream(se.stream_handle(), device=dev)
-    copied = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    c_start = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     free = [torch.cuda.Event() for _ in range(2)]
     free_used = [False, False]
-    copy_ms = []
-    comp = {}       # tick -> (start, end) events on the engine stream
+    cev = {}        # tick -> (start, end) events of its own H2D copy on the copy stream
+    comp = {}       # tick -> (start, end) events of its kernels on the engine stream
 
     def copy(t):
         b = t % 2
         with torch.cuda.stream(cs):
             if free_used[b]:
                 cs.wait_event(free[b])          # the gate of tick t-2 has read this staging buffer
-            c_start[b].record(cs)
+            c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            c0.record(cs)
             stage[b].copy_(host[t * 1600: t * 1600 + per], non_blocking=True)
-            copied[b].record(cs)
+            c1.record(cs)
+            cev[t] = (c0, c1)
 
     events = []
 
@@ -685,7 +685,7 @@ def streaming_host_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, ri
             b = t % 2
             if t + 1 < t0 + nt:
                 copy(t + 1)                     # the next tick's DMA, ahead of this tick's kernels
-            es_.wait_event(copied[b])
+            es_.wait_event(cev[t][1])
             if timed:   # the engine stream starts the tick once its copy and the previous tick are done
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(es_)
@@ -696,14 +696,6 @@ def streaming_host_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, ri
             free[b].record(es_)
             free_used[b] = True
             events.append(se.poll(lagged=True))
-            if timed and t > t0:                # the previous copy has surely finished by now
-                pb = (t - 1) % 2
-                copied[pb].synchronize()
-                copy_ms.append(c_start[pb].elapsed_time(copied[pb]))
-        if timed:   # the last tick's copy
-            pb = (t0 + nt - 1) % 2
-            copied[pb].synchronize()
-            copy_ms.append(c_start[pb].elapsed_time(copied[pb]))
         events.append(se.poll())
 
     run(0, prefill, False)
@@ -718,10 +710,14 @@ def streaming_host_bench(torch, dev, eng_mod, n_streams, n_ticks, seed, word, ri
     ev = np.concatenate(events)
     real = ev[(ev["flags"] & 1) == 0]
     per_tick = wall / n_ticks
-    h2d = float(np.median(copy_ms)) if copy_ms else None
     # a tick's latency from its PCM in host memory to its detections: its own H2D copy, then
-    # its kernels (in real time the copy starts when the block arrives and nothing queues)
-    comp_ms = [comp[t][0].elapsed_time(comp[t][1]) for t in range(prefill, prefill + n_ticks)]
+    # its kernels (in real time the copy starts when the block arrives and nothing queues);
+    # both from that tick's own event pairs (one shared pair per staging buffer was
+    # re-recorded by the next copy before it was read)
+    ticks = range(prefill, prefill + n_ticks)
+    copy_ms = [cev[t][0].elapsed_time(cev[t][1]) for t in ticks]
+    comp_ms = [comp[t][0].elapsed_time(comp[t][1]) for t in ticks]
+    h2d = float(np.median(copy_ms)) if copy_ms else None
     lat = tick_stats([c + k for c, k in zip(copy_ms, comp_ms)])
     lat["compute_ms_max"] = float(max(comp_ms)) if comp_ms else None
     out = {"streams": n_streams, "resident": False, "ingest": "pinned host -> HBM DMA every tick (copy stream, "

@@ -14,7 +14,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 SOURCES = ["ewk_mfcc.hip", "ewk_gate.hip", "ewk_level3.hip", "ewk_gather.hip", "ewk_engine.cpp", "ewk_tables.cpp"]
-HEADERS = ["ewk_internal.h", "ewk_gate.h", "ewk_fp4.h", "ewk_fp4_mel.h", "ewk_rescore.h", "ewk_db64.h", os.path.join("..", "..", "include", "ewk.h")]
+HEADERS = ["ewk_internal.h", "ewk_gate.h", "ewk_rescore.h", "ewk_db64.h", os.path.join("..", "..", "include", "ewk.h")]
 LIB = os.path.join(HERE, "libewk.so")
 ARCH = os.environ.get("EWK_OFFLOAD_ARCH", "gfx950")
 # Per-source flags.  The scorer is VALU-issue bound: SLP-packed f32 ops (v_pk_add_f32)

@@ -6,7 +6,6 @@
 #include <stdint.h>
 
 #include "../../include/ewk.h"
-#include "ewk_fp4_mel.h"
 
 namespace ewk {
 
@@ -31,21 +30,6 @@ constexpr int WAVES = EWK_WAVES;   // waves per scorer workgroup (one workgroup 
 // the two frames a 16-lane group untangles side by side (fr, fr + 4) land 8 banks apart
 __host__ __device__ constexpr int scr_frame_off(int fr) { return fr * SCR_FRAME + 8 * (fr >> 2); }
 
-// Maps of the four-lanes-per-frame pass (ewk_fp4.h; scripts/fp4_model.py): the DFT64 output
-// k'' that slot q of row g holds after the row transposition, and the factoring of the
-// W64^(j k2) twiddles (form A: m (1 - i f), m = cos, f = tan; form B: m (f - i), m = sin, f = cot).
-__host__ __device__ constexpr int f4_sigma0(int q) { return q < 8 ? q : (q < 15 ? q + 1 : 8); }
-__host__ __device__ constexpr int f4_item(int g, int q) {
-    return g == 0 ? 4 * f4_sigma0(q)
-                  : (g == 2 ? 4 * q + 2 : (g == 1 ? 4 * q + (q < 8 ? 1 : 3) : 4 * q + (q < 8 ? 3 : 1)));
-}
-__host__ __device__ constexpr bool f4_formA(int jk) { return (jk % 32) <= 8 || (jk % 32) >= 24; }
-// bin whose (cos, tan)(2 pi k / 512) untangle pair j = 4 q + k' of row g uses (row 0, q = 0:
-// bins 64/192, 32/224, 96/160 and 128)
-__host__ __device__ constexpr int f4_untangle_bin(int g, int j) {
-    return (g == 0 && j < 4) ? (j == 0 ? 64 : (j == 1 ? 32 : (j == 2 ? 96 : 128))) : f4_item(g, j >> 2) + 64 * (j & 3);
-}
-
 // Host-built constant tables (ewk_tables.cpp); copied to LDS by every workgroup.
 struct Tables {
     float2 win2[256];        // (w[2n], w[2n+1]) periodic Hann, n = 0..255
@@ -57,14 +41,6 @@ struct Tables {
     float wpad[MEL_ITERS * 16];
     float dct[NMFCC * NMEL]; // DCT-II ortho rows 0..19
     int32_t ok;              // every band fits its compile-time group width
-    // the four-lanes-per-frame pass (ewk_fp4.h)
-    float2 win4[4][64];      // [r][16 n1 + 4 a + c] = (w[2r + 8n'], w[2r + 8n' + 1]), n' = n1 + 4 (a + 4 c)
-    float tw64[16][12];      // [k2][4 (j - 1)] = (m, -m, f, -f) of W64^(j k2), j = 1..3 (f4_formA)
-    float4 tw4[4][16][3];    // [g][q][s - 1] = (-s, s, c, c) of W256^(s f4_item(g, q)) = c + i s
-    float2 utc[4][32];       // [g][j] = (-cos, cos)(2 pi f4_untangle_bin(g, j) / 512)
-    float2 utt[4][32];       // [g][j] = (t, t), t = tan(2 pi f4_untangle_bin(g, j) / 512)
-    float melw4[4][F4_NINC]; // [g][e]: 0.25 x librosa weight of incidence e's band on row g's bin
-    int32_t ok4;             // the incidence list covers every non-zero weight of the basis
 };
 
 // fp64 path tables (rescoring / reference precision).
@@ -82,6 +58,10 @@ struct Tables64 {
 };
 
 void build_tables(Tables* t);
+// the builders build_tables uses (also linked by scripts/probes/fp4_probe.hip)
+void table_window(double* w /* [512] */);
+void table_mel(float* w /* [128][257] */);
+void table_dct(double* d /* [20][128] */);
 void build_tables64(Tables64* t);
 
 // fp64 re-score (csrc/ewk_rescore.h).  A segment the float32 pass cannot decide alone is

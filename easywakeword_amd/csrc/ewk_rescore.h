@@ -898,10 +898,11 @@ __device__ void tick_end(const ScoreArgs& a, const TickPre* pre = nullptr) {
         *a.work = 0;
 #pragma unroll
         for (int i = 0; i < kRsCtl; ++i) a.rs_ctl[i] = 0;
-        if (!pre) __threadfence();
+        // (no fence: every workgroup of this launch has counted out, so the readers of these
+        // counters are later launches, and the launch's end releases them)
     }
     if (RING && a.mirror) {   // poll mirror: the bank's counters and first events -> pinned host memory
-        __syncthreads();   // this workgroup's re-score writes are done and fenced by thread 0
+        __syncthreads();   // this workgroup's own re-score writes (its second drain) are done
         const volatile int32_t* vc = a.evc;
         const uint4 c = pre ? pre->c : make_uint4((uint32_t)vc[0], (uint32_t)vc[1], (uint32_t)vc[2], (uint32_t)vc[3]);
         const int32_t n = (int32_t)min(min((uint32_t)(c.x - (uint32_t)a.ev_base0), (uint32_t)a.n_seg),
@@ -961,11 +962,22 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem) {
         finished = rs_drain<RING>(ra, smem, wave, lane, true);
     }
     if (lane == 0) flag[1 + wave] = finished;
+    // Hand-off of the finished slots' scores (rs_finish: plain stores) to the last workgroup's
+    // poll-mirror copy (tick_end), MI355X_MICROARCH.md "Valid forms": every storing wave's
+    // stores are acknowledged before the barrier, thread 0 releases (L2 write-back) and WAITS
+    // for the write-back before its count -- the compiler drops that wait after buffer_wbl2
+    // when the scoreboard looks empty (round 5's ISA: `buffer_wbl2 sc1; buffer_inv sc1;
+    // global_atomic_add`, so the count could overtake the write-back and the mirror copy read
+    // a re-scored event's float32 score) -- and each wave of the last workgroup acquires.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
         int any = 0;
         for (int w = 0; w < RS_NW; ++w) any |= flag[1 + w];
-        if (any) __threadfence();
+        if (any) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
         flag[0] = __hip_atomic_fetch_add(&a.rs_ctl[3], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
                   (int)gridDim.x - 1;
     }
@@ -974,7 +986,9 @@ __device__ void score_tail(const ScoreArgs& a, unsigned char* smem) {
 #ifdef EWK_RS_TIMING
     const unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
 #endif
-    __threadfence();   // acquire what every other workgroup released before its count
+    // acquire what every other workgroup released before its count (each wave: its own loads)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // the last workgroup: every other has drained and counted out
     if (threadIdx.x == 0) flag[1 + RS_NW] = rs_pending(ra, false);
     __syncthreads();

@@ -133,57 +133,6 @@ static void mel_read_shifts(const int* lo, const int* n, const int* gw, int* shi
     }
 }
 
-// Tables of the four-lanes-per-frame pass (ewk_fp4.h; scripts/fp4_model.py is the model).
-static void build_tables_fp4(Tables* t, const double* w, const float* mel) {
-    for (int r = 0; r < 4; ++r)   // [r][n1][a][c]: column a of DFT16 block n1 reads 32 contiguous bytes
-        for (int n1 = 0; n1 < 4; ++n1)
-            for (int a = 0; a < 4; ++a)
-                for (int c = 0; c < 4; ++c) {
-                    const int np = n1 + 4 * (a + 4 * c);
-                    t->win4[r][16 * n1 + 4 * a + c] = make_float2((float)w[2 * r + 8 * np], (float)w[2 * r + 8 * np + 1]);
-                }
-    for (int k2 = 1; k2 < 16; ++k2)
-        for (int j = 1; j <= 3; ++j) {   // W64^(j k2) = m (1 - i f) (form A) or -i m (1 + i f) (form B)
-            const int jk = j * k2;
-            const double ph = 2.0 * kPi * jk / 64.0;
-            const bool a = f4_formA(jk);
-            const float m = (float)(a ? cos(ph) : sin(ph)), f = (float)(a ? tan(ph) : cos(ph) / sin(ph));
-            float* e = &t->tw64[k2][4 * (j - 1)];
-            e[0] = m; e[1] = -m; e[2] = f; e[3] = -f;
-        }
-    for (int g = 0; g < 4; ++g)
-        for (int q = 0; q < 16; ++q)
-            for (int s = 1; s <= 3; ++s) {
-                const double ph = 2.0 * kPi * s * f4_item(g, q) / 256.0;
-                const float c = (float)cos(ph), sn = (float)-sin(ph);
-                t->tw4[g][q][s - 1] = make_float4(-sn, sn, c, c);
-            }
-    for (int g = 0; g < 4; ++g)
-        for (int j = 0; j < 32; ++j) {
-            const double ph = 2.0 * kPi * f4_untangle_bin(g, j) / 512.0;   // cos is never 0 in float (k = 128: 6.1e-17)
-            const float c = (float)cos(ph);
-            t->utc[g][j] = make_float2(-c, c);
-            t->utt[g][j] = make_float2((float)(sin(ph) / cos(ph)), (float)(sin(ph) / cos(ph)));
-        }
-    // per-row weights of the incidence list; every non-zero weight must be covered
-    bool covered[NMEL][NBIN] = {};
-    for (int G = 0; G < 4; ++G)
-        for (int e = F4_INC_START[G]; e < F4_INC_START[G + 1]; ++e) {
-            const bool real = e < F4_INC_START[G] + F4_INC_COUNT[G];
-            const int m = 32 * G + F4_INC_BAND[e], slot = F4_INC_SLOT[e];
-            for (int g = 0; g < 4; ++g) {
-                const int b = f4_item(g, slot >> 2) + 64 * (slot & 3);
-                const float wv = real ? mel[m * NBIN + b] : 0.0f;
-                t->melw4[g][e] = 0.25f * wv;
-                if (real && wv != 0.0f) covered[m][b] = true;
-            }
-        }
-    t->ok4 = 1;
-    for (int m = 0; m < NMEL; ++m)
-        for (int b = 0; b < NBIN; ++b)
-            if (mel[m * NBIN + b] != 0.0f && !covered[m][b]) t->ok4 = 0;
-}
-
 void build_tables(Tables* t) {
     memset(t, 0, sizeof(*t));
     double w[NFFT];
@@ -228,7 +177,6 @@ void build_tables(Tables* t) {
     double d[NMFCC * NMEL];
     dct_rows(d);
     for (int i = 0; i < NMFCC * NMEL; ++i) t->dct[i] = (float)d[i];
-    build_tables_fp4(t, w, mel.data());
 }
 
 void build_tables64(Tables64* t) {
@@ -261,5 +209,9 @@ void build_tables64(Tables64* t) {
     }
     t->mel_off[NMEL] = off;
 }
+
+void table_window(double* w) { hann_periodic(w); }
+void table_mel(float* w) { mel_dense(w); }
+void table_dct(double* d) { dct_rows(d); }
 
 }  // namespace ewk

@@ -11,8 +11,9 @@ for f in easywakeword_amd/csrc/ewk_gather.hip; do   # sources that older revisio
   if [ "$REV" = "WT" ] || git -C "$R" cat-file -e "$REV:$f" 2>/dev/null; then SRCS="$SRCS $(basename $f)"; fi
 done
 HDRS="ewk_internal.h ewk_gate.h"
-for h in ewk_rescore.h ewk_fp4.h ewk_fp4_mel.h ewk_db64.h; do   # headers that older revisions lack
-  if [ "$REV" = "WT" ] || git -C "$R" cat-file -e "$REV:easywakeword_amd/csrc/$h" 2>/dev/null; then HDRS="$HDRS $h"; fi
+for h in ewk_rescore.h ewk_fp4.h ewk_fp4_mel.h ewk_db64.h; do   # headers that some revisions lack (ewk_fp4*.h: round 5 only)
+  if { [ "$REV" = "WT" ] && [ -f "$R/easywakeword_amd/csrc/$h" ]; } || \
+     { [ "$REV" != "WT" ] && git -C "$R" cat-file -e "$REV:easywakeword_amd/csrc/$h" 2>/dev/null; }; then HDRS="$HDRS $h"; fi
 done
 for s in $SRCS $HDRS; do
   f=easywakeword_amd/csrc/$s

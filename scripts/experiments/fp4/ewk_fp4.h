@@ -1,4 +1,6 @@
-// ewk_fp4.h -- the frame pass of the float32 scorer (round 5): four lanes per frame.
+// ewk_fp4.h -- a frame pass of the float32 scorer built in round 5: four lanes per frame.
+// Measured slower than the product pass ("Round 5") and kept here, out of
+// libewk.so; scripts/probes/fp4_probe.hip builds it.
 //
 // Replaces the FFT + mel + log of WordMatcher.extract_mfcc's librosa call (reference
 // easywakeword/wakeword.py:561-563: stft(n_fft=512, hop=160, center=True) -> |.|^2 -> Slaney
@@ -27,8 +29,9 @@
 // one instruction per complex add, two per complex multiply.
 #pragma once
 
+#include "../../../easywakeword_amd/csrc/ewk_internal.h"
 #include "ewk_fp4_mel.h"
-#include "ewk_internal.h"
+#include "fp4_tables.h"
 
 namespace ewk {
 namespace fp4 {
@@ -197,7 +200,7 @@ __device__ __forceinline__ f2 tw_mul(bool A, f2 M, f2 up) { return A ? F4_B0(M) 
 __device__ __forceinline__ f2 cmul4(f2 a, f4 W) { return fma2(F4_SW(a), W.xy, a * F4_B0(W.zw)); }
 
 // ---- LDS table fill (once per workgroup) -------------------------------------------------
-__device__ __forceinline__ void fill_tables(const Tables* __restrict__ tab, unsigned char* t, float win_scale, int tid,
+__device__ __forceinline__ void fill_tables(const Fp4Tables* __restrict__ tab, unsigned char* t, float win_scale, int tid,
                                             int nthreads) {
     for (int i = tid; i < 4 * 64; i += nthreads) {
         const int r = i >> 6, e = i & 63;

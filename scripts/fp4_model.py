@@ -4,7 +4,7 @@ A wave holds 16 frames x 4 rows: lane = p + 16 r (p = frame of the pass, r = row
 model replays, for one frame, what the four lanes of a frame hold at every step, in float64,
 and checks the power spectrum, the mel band energies and the band -> DCT-slot map against
 numpy.  It also prints the tables' sizes and the mel incidence count the kernel unrolls.
-The HIP code (easywakeword_amd/csrc/ewk_fp4.h) and the host tables (ewk_tables.cpp,
+The HIP code (scripts/experiments/fp4/ewk_fp4.h) and the host tables (ewk_tables.cpp,
 build_tables) follow the same maps; tests/test_fp4_tables.py checks the C++ tables against
 the functions below.
 
@@ -153,7 +153,7 @@ if __name__ == "__main__":
 
 
 def emit_header(path: str) -> None:
-    """easywakeword_amd/csrc/ewk_fp4_mel.h: the mel incidence list the kernel unrolls."""
+    """scripts/experiments/fp4/ewk_fp4_mel.h: the mel incidence list the kernel unrolls."""
     from oracle import mfcc_ref
     W = mfcc_ref.mel_filterbank().astype(np.float64)
     inc = mel_incidence(W)

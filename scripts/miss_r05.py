@@ -1,0 +1,189 @@
+"""Round-6 investigation of the round-5 one-off ring-path score miss (CPU only, oracle).
+
+Round 5's full GPU session reported, in tests/test_gpu_gate.py::test_many_streams_vs_oracle,
+stream 1 / tick 164 scored 98.3817 by the engine against the oracle's 98.0476.  The scenario
+is seeded, so everything here replays it on the CPU:
+
+  1. every oracle event of the 32 streams with its score -- is 98.3817 another event's score
+     (a slot -> segment mapping error)?
+  2. plausible corruptions of the event's input, each scored with the oracle:
+     - part of the window taken one ring wrap (100 ticks) earlier (stale ring lines),
+     - the window shifted by +-k ticks / +-k samples,
+     - one 16-frame tile (2,560 samples) zeroed, duplicated from a neighbour, or clamped at a
+       wrong top_db threshold,
+     - a truncated / extended segment (length off by 1..n frames).
+
+Usage: python scripts/miss_r05.py [target]   (target default 98.3817)
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "tests"))
+sys.path.insert(0, os.path.join(HERE, ".."))
+
+import synth  # noqa: E402
+from golden_io import matcher_fixture, template_arrays  # noqa: E402
+from oracle import mfcc_ref  # noqa: E402
+from oracle.gate_ref import GateConfig, run_stream  # noqa: E402
+
+TARGET = float(sys.argv[1]) if len(sys.argv) > 1 else 98.3817
+ORACLE = 98.0476
+
+
+def scenario():
+    n = 32
+    pcms = []
+    for i in range(n):
+        rng = np.random.default_rng(500 + i)
+        p, _ = synth.make_stream(seed=2000 + i, n_words=4, sigma=float(rng.uniform(1e-4, 5e-3)),
+                                 gain=float(rng.uniform(0.2, 3.0)), distractors=bool(i % 2))
+        pcms.append(p)
+    L = min(len(p) for p in pcms)
+    L -= L % 1600
+    return np.stack([p[:L] for p in pcms]).astype(np.float32)
+
+
+def score(tm, ts, x):
+    cm, cs = mfcc_ref.extract_mfcc(np.asarray(x, np.float64))
+    return float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs)), cm, cs
+
+
+def score_stats(tm, ts, cm, cs):
+    return float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
+
+
+def main():
+    fx, _ = matcher_fixture()
+    tm, ts = template_arrays(fx)
+    data = scenario()
+    gate = GateConfig(pre_speech_silence=0.8, speech_duration_min=0.3, speech_duration_max=2.0,
+                      post_speech_silence=0.4)
+    print(f"scenario: {data.shape[0]} streams x {data.shape[1]} samples ({data.shape[1] // 1600} ticks)")
+    allev = []
+    for i in range(data.shape[0]):
+        for e in run_stream(data[i], gate).events:
+            if e.skipped:
+                continue
+            s, cm, _ = score(tm, ts, e.audio)
+            allev.append((i, e.tick, e.length, s, float(np.linalg.norm(cm)), e))
+    print(f"{len(allev)} scored oracle events")
+    print("\n1. oracle scores nearest the target", TARGET)
+    for i, tick, ln, s, mn, _ in sorted(allev, key=lambda r: abs(r[3] - TARGET))[:6]:
+        print(f"   stream {i:2d} tick {tick:4d} L {ln:6d} |mean| {mn:7.1f} score {s:.4f}  d {s - TARGET:+.4f}")
+    ev = [r for r in allev if r[0] == 1 and r[1] == 164]
+    if not ev:
+        print("no oracle event at stream 1 tick 164")
+        return
+    _, tick, ln, s0, mn, e = ev[0]
+    print(f"\nthe event: stream 1 tick {tick} length {ln} |mean| {mn:.1f} oracle score {s0:.6f}")
+    x = data[1].astype(np.float64)
+    end = tick * 1600                      # samples delivered through this tick
+    # the segment is the last `ln` samples of the request window ending some e samples before end
+    seg = np.asarray(e.audio, np.float64)
+    # locate the segment in the stream
+    pos = None
+    for cand in range(end - 48000 - 3200, end + 1):
+        if cand >= 0 and cand + ln <= len(x) and x[cand] == seg[0] and np.array_equal(x[cand:cand + ln], seg):
+            pos = cand
+            break
+    print(f"   segment = stream samples [{pos}, {pos + ln}) (end of tick {tick}: {end})")
+    results = []
+
+    def rec(name, y):
+        sc, _, _ = score(tm, ts, y)
+        results.append((abs(sc - TARGET), name, sc))
+
+    # 2a. stale ring lines: part of the window from one wrap (100 ticks = 160000 samples) earlier
+    wrap = 160000
+    for a in range(0, ln, 1600):
+        for w in (16, 32, 64, 128, 256, 512, 1024, 1600):
+            y = seg.copy()
+            s_abs = pos + a
+            b = min(ln, a + w)
+            if s_abs - wrap >= 0:
+                y[a:b] = x[s_abs - wrap:pos + b - wrap]
+                rec(f"stale wrap [{a},{b})", y)
+    # stale: the ring's content before this tick's samples were written (the tick's 1600 at ring pos)
+    for k in range(1, 17):
+        t0 = (tick - k + 1) * 1600 - 1600     # start of tick (tick-k+1)'s block in stream samples
+        a, b = t0 - pos, t0 - pos + 1600
+        if b <= 0 or a >= ln:
+            continue
+        y = seg.copy()
+        aa, bb = max(a, 0), min(b, ln)
+        y[aa:bb] = x[pos + aa - wrap:pos + bb - wrap]
+        rec(f"tick {tick - k + 1} block stale (one wrap old)", y)
+        y = seg.copy()
+        y[aa:bb] = 0.0
+        rec(f"tick {tick - k + 1} block zero", y)
+    # 2b. shifted windows
+    for d in list(range(-32, 33)) + [k * 1600 for k in range(-4, 5)] + [k * 160 for k in range(-8, 9)]:
+        if d == 0:
+            continue
+        if pos + d < 0 or pos + d + ln > len(x):
+            continue
+        rec(f"shift {d:+d}", x[pos + d:pos + d + ln])
+    for d in range(-1600, 1601, 160):
+        if d == 0:
+            continue
+        rec(f"length {d:+d}", x[pos:pos + ln + d])
+        rec(f"start {d:+d} same end", x[pos + d:pos + ln])
+    # 2c. tile-level corruptions: tiles of 16 frames = 2,560 samples of hop
+    T = 1 + ln // 160
+    nt = (T + 15) // 16
+    S, logmel = mfcc_frames(seg)
+    for t in range(nt):
+        f0, f1 = 16 * t, min(T, 16 * t + 16)
+        # drop tile t's frames from the statistics
+        keep = np.r_[0:f0, f1:T]
+        results.append(stat_case(tm, ts, logmel, keep, f"tile {t} dropped"))
+        # duplicate tile t in place of its neighbour
+        for u in range(nt):
+            if u == t:
+                continue
+            g0, g1 = 16 * u, min(T, 16 * u + 16)
+            if g1 - g0 != f1 - f0:
+                continue
+            idx = np.arange(T)
+            idx[g0:g1] = np.arange(f0, f1)
+            results.append(stat_case(tm, ts, logmel, idx, f"tile {u} := tile {t}"))
+        # tile t clamped at a wrong threshold (its own max - 80, or not clamped)
+        for name, thr in (("unclamped", -np.inf), ("own max-80", logmel[:, f0:f1].max() - 80.0)):
+            results.append(stat_case(tm, ts, logmel, np.arange(T), f"tile {t} {name}", tile=(f0, f1, thr)))
+    # the whole segment clamped wrong
+    mx = logmel.max()
+    for dthr in (-10, -5, -1, 1, 5, 10, 20, 40):
+        results.append(stat_case(tm, ts, logmel, np.arange(T), f"global thr {dthr:+d} dB", glob=mx - 80.0 + dthr))
+    results.sort()
+    print(f"\n2. corruptions nearest {TARGET} ({len(results)} tried)")
+    for d, name, sc in results[:15]:
+        print(f"   {name:40s} {sc:.4f}  d {sc - TARGET:+.4f}")
+
+
+def mfcc_frames(seg):
+    """log-mel (dB, unclamped) of the oracle, [128][T]."""
+    mel_basis, _ = mfcc_ref._tables()
+    S = np.einsum("...ft,mf->...mt", mfcc_ref.power_spectrogram(seg), mel_basis, optimize=True)
+    db = 10.0 * np.log10(np.maximum(1e-10, S))
+    return S, db
+
+
+def stat_case(tm, ts, db, idx, name, tile=None, glob=None):
+    import scipy.fft
+    d = db.copy()
+    thr = d.max() - 80.0 if glob is None else glob
+    d = np.maximum(d, thr)
+    if tile is not None:
+        f0, f1, t = tile
+        d[:, f0:f1] = np.maximum(db[:, f0:f1], t)
+    d = d[:, idx]
+    c = scipy.fft.dct(d, type=2, norm="ortho", axis=0)[:20]
+    sc = score_stats(tm, ts, c.mean(axis=1), c.std(axis=1))
+    return (abs(sc - TARGET), name, sc)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,4 +1,4 @@
-// fp4_probe.hip -- the four-lanes-per-frame pass (csrc/ewk_fp4.h) alone: log-mel values of
+// fp4_probe.hip -- the four-lanes-per-frame pass (scripts/experiments/fp4/ewk_fp4.h) alone: log-mel values of
 // every frame of a batch of equal-length segments (check mode), or timed passes (time mode).
 //
 //   fp4_probe check <pcm.f32> <n_seg> <len> <out.f32>       -> out[seg][t][128] (dB, no top_db)
@@ -14,7 +14,7 @@
 
 #include <vector>
 
-#include "../../easywakeword_amd/csrc/ewk_fp4.h"
+#include "../experiments/fp4/ewk_fp4.h"
 
 using namespace ewk;
 
@@ -33,7 +33,7 @@ constexpr int PROBE_LDS_MIN = fp4::TABLE_BYTES + NW * fp4::STAGE_BYTES;
 constexpr int PROBE_LDS = PROBE_LDS_MIN > 82 * 1024 ? PROBE_LDS_MIN : 82 * 1024;
 
 template <int MODE>   // 0 check (write log-mel), 1 time (checksum), 2 time with DCT, 3 check MFCC (pass + DCT)
-__global__ __launch_bounds__(64 * NW, 1) void k_probe(const Tables* __restrict__ tab, const float* __restrict__ pcm,
+__global__ __launch_bounds__(64 * NW, 1) void k_probe(const Fp4Tables* __restrict__ tab, const float* __restrict__ pcm,
                                                       int n_seg, int len, int* work, float* out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     fp4::fill_tables(tab, smem, 1.0f, threadIdx.x, blockDim.x);
@@ -127,15 +127,15 @@ int main(int argc, char** argv) {
     if (argc < 2) return 1;
     const bool mfcc = !strcmp(argv[1], "mfcc");
     const bool check = !strcmp(argv[1], "check") || mfcc;
-    Tables* ht = (Tables*)calloc(1, sizeof(Tables));
-    build_tables(ht);
-    if (!ht->ok || !ht->ok4) {
-        fprintf(stderr, "tables not ok (%d %d)\n", ht->ok, ht->ok4);
+    Fp4Tables* ht = (Fp4Tables*)calloc(1, sizeof(Fp4Tables));
+    build_tables_fp4(ht);
+    if (!ht->ok4) {
+        fprintf(stderr, "tables not ok\n");
         return 3;
     }
-    Tables* dt;
-    CK(hipMalloc(&dt, sizeof(Tables)));
-    CK(hipMemcpy(dt, ht, sizeof(Tables), hipMemcpyHostToDevice));
+    Fp4Tables* dt;
+    CK(hipMalloc(&dt, sizeof(Fp4Tables)));
+    CK(hipMemcpy(dt, ht, sizeof(Fp4Tables), hipMemcpyHostToDevice));
     int n_seg, len;
     std::vector<float> pcm;
     if (check) {

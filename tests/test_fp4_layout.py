@@ -1,4 +1,4 @@
-"""CPU checks of the four-lanes-per-frame pass's index algebra (easywakeword_amd/csrc/ewk_fp4.h).
+"""CPU checks of the four-lanes-per-frame pass's index algebra (scripts/experiments/fp4/ewk_fp4.h).
 
 scripts/fp4_model.py replays, in float64, what the four lanes of a frame hold at every step
 (row transposition, untangle pairs, mel incidences, reduce-scatter) -- these tests pin it:
@@ -44,5 +44,5 @@ def test_lane_algorithm_power_and_mel():
 def test_generated_header_is_current(tmp_path):
     out = tmp_path / "ewk_fp4_mel.h"
     fp4_model.emit_header(str(out))
-    cur = open(os.path.join(ROOT, "easywakeword_amd", "csrc", "ewk_fp4_mel.h")).read()
+    cur = open(os.path.join(ROOT, "scripts", "experiments", "fp4", "ewk_fp4_mel.h")).read()
     assert out.read_text() == cur

@@ -94,18 +94,25 @@ def test_many_streams_vs_oracle(template):
         got.extend(eng.poll().tolist())
     tm, ts = template
     n_ev = 0
+    bad = []   # every mismatch, not the first: the evidence is dumped before the test fails
     for i in range(n):
         ref = _oracle_events(data[i], gate)
         mine = sorted([g for g in got if g[0] == i], key=lambda g: g[2])
-        assert [(g[2], g[1], bool(g[7] & 1)) for g in mine] == [(e.tick, e.length, e.skipped) for e in ref], i
+        if [(g[2], g[1], bool(g[7] & 1)) for g in mine] != [(e.tick, e.length, e.skipped) for e in ref]:
+            bad.append(dict(stream=i, why="identity", mine=mine, want=[(e.tick, e.length, e.skipped) for e in ref]))
+            continue
         for g, e in zip(mine, ref):
             if e.skipped:
                 continue
             cm, cs = mfcc_ref.extract_mfcc(e.audio)
             s = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
-            assert score_close(g[5], s, 1e-4), (i, g, s)
-            assert bool(g[6]) == (s >= 75.0)
+            if not score_close(g[5], s, 1e-4) or bool(g[6]) != (s >= 75.0):
+                bad.append(dict(stream=i, why="score", mine=g, oracle=s))
             n_ev += 1
+    if bad:
+        from evidence import dump
+        path = dump("many_streams", dict(bad=bad, events=got))
+        pytest.fail(f"{len(bad)} mismatches (evidence {path}): {bad[:4]}")
     assert n_ev > 20
 
 
