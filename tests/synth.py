@@ -208,3 +208,34 @@ def fuzz_segments(seed: int, n: int, word: np.ndarray) -> list:
             x[2560:5120] = x[0:2560]
         segs.append(x)
     return segs
+
+
+MEAN_BAND_KINDS = ("white", "pink", "tone_noise", "word_noise")
+
+
+def mean_band_segment(kind: str, seed: int, gain: float, length: int) -> np.ndarray:
+    """Loud segments of four recipes other than the streaming bench's, for the vanishing-mean
+    criterion's evidence (tests/golden/make_mean_band.py picks parameters
+    whose oracle MFCC mean vector has |mean| in [32, 64)): white noise, pink (1/f power) noise,
+    a tone plus white noise, and the reference word (looped, x 4) in white noise.  (High-passed
+    noise and a clipped word never get there: their spectral shape alone keeps |mean| above
+    ~110.)  Deterministic in (kind, seed, gain, length)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n = int(length)
+    if kind == "white":
+        x = rng.standard_normal(n) * gain
+    elif kind == "pink":
+        w = np.fft.rfft(rng.standard_normal(n))
+        f = np.arange(len(w), dtype=np.float64)
+        f[0] = 1.0
+        x = np.fft.irfft(w / np.sqrt(f), n) * gain * np.sqrt(n / 16.0)
+    elif kind == "tone_noise":
+        t = np.arange(n) / SR
+        f0 = float(rng.uniform(150.0, 3000.0))
+        x = gain * (np.sin(2 * np.pi * f0 * t) + 0.3 * rng.standard_normal(n))
+    elif kind == "word_noise":
+        word = load_word().astype(np.float64)
+        x = 4.0 * np.resize(word, n) + gain * rng.standard_normal(n)
+    else:
+        raise ValueError(kind)
+    return x.astype(np.float32)

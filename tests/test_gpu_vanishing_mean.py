@@ -125,3 +125,39 @@ def test_vanishing_mean_wakeword_facade(streams, template):
     assert len(ev) == len(run_stream(pcm, GateConfig(**GATE)).events)
     tm, ts = ww._matcher.reference_mfcc_mean, ww._matcher.reference_mfcc_std
     assert _check(ev, pcm, (tm, ts), threshold=101.0) >= 1   # the facade's threshold: nothing matches
+
+
+def test_mean_band_four_recipes_vs_oracle():
+    """600 segments whose ORACLE |mean| lies in [32, 64) -- the band the
+    round-5 criterion (|mean| < 32) no longer re-scores -- from four recipes other than the
+    streaming bench's (tests/golden/mean_band_cases.json, made by make_mean_band.py: loud white
+    and pink noise, a tone plus noise, the word in loud noise), scored by the linear batch
+    scorer (float64 candidates).  Every score within 1e-4 of the oracle with the same decision;
+    the worst error per recipe goes to gpurun_out/ (the criterion's evidence)."""
+    import json
+    import os
+    from easywakeword_amd import Engine
+    from evidence import dump
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mean_band_cases.json")) as f:
+        cases = json.load(f)["cases"]
+    segs = [synth.mean_band_segment(c["kind"], c["seed"], c["gain"], c["length"]) for c in cases]
+    eng = Engine()
+    eng.template_from_pcm(synth.load_word())
+    m, _, sc, mt = eng.score(segs, candidate_dtype="float64")
+    ref = np.array([c["score"] for c in cases])
+    d = np.abs(sc - ref)
+    kinds = sorted(set(c["kind"] for c in cases))
+    per = {}
+    for k in kinds:
+        sel = np.array([c["kind"] == k for c in cases])
+        j = int(np.argmax(np.where(sel, d, -1.0)))
+        per[k] = dict(n=int(sel.sum()), max_err=float(d[sel].max()), median_err=float(np.median(d[sel])),
+                      worst=dict(cases[j], gpu=float(sc[j])),
+                      gpu_listed=int((np.linalg.norm(m[sel], axis=1) < RESCORE_TINY_MEAN).sum()))
+    dump("mean_band", dict(criterion=RESCORE_TINY_MEAN, max_err=float(d.max()), per_recipe=per,
+                           err_by_mean=[[c["mean_norm"], float(e)] for c, e in zip(cases, d)]))
+    print("mean band [32, 64):", {k: (v["n"], v["max_err"]) for k, v in per.items()})
+    assert len(kinds) >= 3 and len(cases) >= 500
+    assert float(d.max()) <= SCORE_TOL, per
+    np.testing.assert_array_equal(mt, ref >= 75.0)
+    eng.close()
