@@ -13,6 +13,8 @@ s on), 10 s prefill + 15 s.  Checks on what rank 0 received:
   tick and length; scores within 1e-4 -- the shards score with the cooperative ring
   scorer, the single engine with one segment per wave, and both send the segments the
   float32 pass cannot decide to the same fp64 re-score -- every one a match);
+* every scored event of that engine (positives and rejects) and every gathered positive
+  is within 1e-4 of the oracle (oracle/mfcc_ref.py) with the oracle's decision;
 * every gathered level-3 PCM equals wakeword.py:1019-1025's numpy normalisation of its
   segment, cut from the signal (bit for bit).
 """
@@ -73,6 +75,7 @@ def test_config4_sharded_positives_equal_one_engine(tmp_path):
     sig = bench.make_shifted_signal(torch, dev, N_TOTAL, TICKS, SEED, word)
     se = ewa.StreamEngine(N_TOTAL)
     se.template_from_pcm(word)
+    se_template = se.get_template()
     evs, t = [], 0
     while t < TICKS:
         nt = min(32 if t < config4_rank.PREFILL else 1, TICKS - t)
@@ -92,8 +95,31 @@ def test_config4_sharded_positives_equal_one_engine(tmp_path):
     assert float(np.max(np.abs(sc - pos["score"][o1]))) <= 1e-4   # MODE 1 vs MODE 2: one fp64 path
     assert np.all(sc >= 75.0)
 
-    # the gathered level-3 PCM: each equals the normalisation of one positive's segment
+    # every scored event of the 65,536 streams (positives and rejects) against the oracle, and
+    # the gathered positives' scores: stream s hears the signal from tick
+    # s on, so events with equal (tick - s, request, length) hold the same samples -- each
+    # distinct segment is scored once by the oracle (tests/oracle_pool.py)
+    from oracle_pool import oracle_scores
     host = sig.cpu().numpy()
+    sc_ev = ev[(ev["flags"] & 1) == 0]
+    n_req = (sc_ev["tick"].astype(np.int64) * 1600 - sc_ev["ring_start"].astype(np.int64)) % RING
+    p0 = sc_ev["tick"].astype(np.int64) * 1600 - n_req                    # offset in the stream
+    key = np.stack([sc_ev["tick"].astype(np.int64) - sc_ev["stream"], n_req, sc_ev["length"].astype(np.int64)], 1)
+    uniq, inv = np.unique(key, axis=0, return_inverse=True)
+    inv = inv.reshape(-1)
+    first = np.zeros(len(uniq), np.int64)
+    first[inv[::-1]] = np.arange(len(sc_ev))[::-1]
+    segs = [host[int(sc_ev["stream"][i]) * 1600 + int(p0[i]):][:int(sc_ev["length"][i])] for i in first]
+    ref = oracle_scores(segs, *se_template)[inv]
+    d = np.abs(sc_ev["score"] - ref)
+    assert np.array_equal(np.isnan(sc_ev["score"]), np.isnan(ref))
+    assert np.nanmax(d) <= 1e-4, (float(np.nanmax(d)), sc_ev[int(np.nanargmax(d))])
+    np.testing.assert_array_equal(sc_ev["match"].astype(bool), ref >= 75.0)
+    ref_pos = {(int(e["stream"]), int(e["tick"])): r for e, r in zip(sc_ev, ref)}
+    gathered = np.array([ref_pos[(int(s), int(tk))] for s, tk in rec[o2, :2]])
+    assert float(np.max(np.abs(sc - gathered))) <= 1e-4 and np.all(gathered >= 75.0)
+
+    # the gathered level-3 PCM: each equals the normalisation of one positive's segment
     ring_start = {(int(e["stream"]), int(e["tick"])): int(e["ring_start"]) for e in pos}
     by_len = {}
     for s, tk, ln, _ in rec:
