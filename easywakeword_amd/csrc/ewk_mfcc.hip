@@ -147,9 +147,11 @@ constexpr int W_BYTES = W_SPEC + (kSpecOrder + kSpecTiles) * 4;
 constexpr int L_WG = L_SHARED_END + WAVES * W_BYTES;    // ring mode: segment index + per-wave log-mel max/min
 constexpr int LDS_BYTES = L_WG + 16 + 8 * WAVES;
 constexpr int kRescoreFrames = 16;
-// |mean vector| below which the fp64 path decides (round 5: 32, was 64 -- the float32 score error
-// scales as ~2.8e-3 / |mean| on streaming events, <= 1.2e-5 observed above 32: DESIGN.md
-// numerics, profiles/r05_v26_mean_err.txt; easywakeword_amd/_lib.py RESCORE_TINY_MEAN mirrors it)
+// |mean vector| below which the fp64 path decides (round 5: 32, was 64).  Evidence for 32: the
+// float32 score error of streaming events is <= 1.2e-5 above |mean| 32 (profiles/r05_v26_mean_err.txt)
+// and 600 segments of four other loud recipes with oracle |mean| in [32, 64) score within 8.6e-6
+// (round 6, profiles/r06_v1_mean_band_evidence.json); DESIGN.md numerics.
+// easywakeword_amd/_lib.py RESCORE_TINY_MEAN mirrors it.
 #ifndef EWK_TINY_MEAN
 #define EWK_TINY_MEAN 32.0
 #endif
