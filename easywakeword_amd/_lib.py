@@ -28,6 +28,10 @@ EWK_EV_RESCORED = 2
 # |MFCC mean vector| below which a segment's score comes from the fp64 re-score (the scorer's
 # kTinyMean, csrc/ewk_mfcc.hip; tests/test_rescore_criteria.py keeps the two equal)
 RESCORE_TINY_MEAN = 32.0
+# ... unless its float32 similarity percent is below -(NAN_MARGIN_A / |mean| + NAN_MARGIN_B): NaN in
+# the reference beyond the float32 error, not re-scored (kNanMarginA / kNanMarginB, same test)
+NAN_MARGIN_A = 0.5
+NAN_MARGIN_B = 0.05
 EWK_PUSH_DEVICE = 1
 EWK_PCM_DEVICE = 1
 EWK_OUT_DEVICE = 4

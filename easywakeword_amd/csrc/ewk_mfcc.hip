@@ -157,6 +157,16 @@ constexpr int kRescoreFrames = 16;
 #endif
 constexpr double kTinyMean = EWK_TINY_MEAN;
                                     // (loud audio, c0 cancelling: DESIGN.md numerics)
+// A vanishing-mean segment whose float32 similarity percent p = 100 (0.7 sm + 0.3 ss) is below
+// -(kNanMarginA / |mean| + kNanMarginB) scores NaN in the reference too (p ** 1.5 of a negative
+// p, wakeword.py:621-625): the float32 pass's error in p is far smaller than that (round 6,
+// scripts/nan_margin.py: DESIGN.md numerics), so the fp64 re-score cannot change its score or
+// decision and the segment is not listed for it.  (Mirrored by _lib.NAN_MARGIN_A / _B.)
+#ifndef EWK_NAN_MARGIN_A
+#define EWK_NAN_MARGIN_A 0.5
+#endif
+constexpr double kNanMarginA = EWK_NAN_MARGIN_A;
+constexpr double kNanMarginB = 0.05;
 constexpr double kTinyStd = 20.0;   // |std vector| below which the fp64 path decides (bench batch >= 24.8,
                                     // streaming events >= 32.5: scripts/std_norm_dist.py)
 static_assert(LDS_BYTES <= 160 * 1024, "the workgroup must fit a CU's LDS");
@@ -1506,11 +1516,11 @@ __device__ double score_f32cand(const float* tm, const float* ts, const float* c
 
 // Fast-path finishes (the fp64 re-score keeps the reference's exact pow / sequential dots).
 __device__ __forceinline__ double score_f64_finish(double uu_m, double uu_s, double uv_m, double vv_m, double uv_s,
-                                                   double vv_s) {
+                                                   double vv_s, double& percent) {
 #pragma clang fp contract(off)
     const double sm = 1.0 - clip02(1.0 - uv_m / sqrt(uu_m * vv_m));
     const double ss = 1.0 - clip02(1.0 - uv_s / sqrt(uu_s * vv_s));
-    const double percent = (sm * 0.7 + ss * 0.3) * 100.0;
+    percent = (sm * 0.7 + ss * 0.3) * 100.0;
     return percent * sqrt(percent) / 10.0;   // p**1.5 (NaN for p < 0 like pow)
 }
 
@@ -1535,7 +1545,7 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, fl
                                                int lane, int seg, int len, float theta_s) {
     bool near = a.list_all;
     if (a.has_template) {
-        double score, std2, mean2;
+        double score, std2, mean2, percent = 0.0;
         if (a.cand_f32) {   // float32 candidates: float products, float-rounded dots (sdot)
             const float uv_m = (float)wave_sum_d((double)(tmf * cmf)), vv_m = (float)wave_sum_d((double)(cmf * cmf));
             const float uv_s = (float)wave_sum_d((double)(tsf * csf)), vv_s = (float)wave_sum_d((double)(csf * csf));
@@ -1545,7 +1555,7 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, fl
         } else {
             const double uv_m = wave_sum_d((double)tmf * (double)cmf), vv_m = wave_sum_d((double)cmf * (double)cmf);
             const double uv_s = wave_sum_d((double)tsf * (double)csf), vv_s = wave_sum_d((double)csf * (double)csf);
-            score = score_f64_finish((double)a.uu_m32, (double)a.uu_s32, uv_m, vv_m, uv_s, vv_s);
+            score = score_f64_finish((double)a.uu_m32, (double)a.uu_s32, uv_m, vv_m, uv_s, vv_s, percent);
             std2 = vv_s;
             mean2 = vv_m;
         }
@@ -1562,13 +1572,15 @@ __device__ __forceinline__ void score_epilogue(const ScoreArgs& a, float cmf, fl
             // becomes a direction error, up to 3.6e-4 in the score; DESIGN.md numerics).  An
             // exactly constant segment keeps its NaN (zero std; the reference's own value there
             // is a rounding artefact).
+            // (float64 candidates only: a vanishing-mean segment that is NaN beyond the float32 error)
+            const bool sure_nan = !a.cand_f32 && percent < -(kNanMarginA / sqrt(mean2) + kNanMarginB);
             near = near || fabs(score - a.threshold) < a.rescore_margin || (1 + len / HOP) <= kRescoreFrames ||
-                   (std2 > 0.0 && std2 < kTinyStd * kTinyStd) || mean2 < kTinyMean * kTinyMean;
+                   (std2 > 0.0 && std2 < kTinyStd * kTinyStd) || (mean2 < kTinyMean * kTinyMean && !sure_nan);
 #ifdef EWK_LIST_STATS
             if (near) {
                 const unsigned long long T = 1 + len / HOP;
                 const bool why[4] = {fabs(score - a.threshold) < a.rescore_margin, (int)T <= kRescoreFrames,
-                                     std2 > 0.0 && std2 < kTinyStd * kTinyStd, mean2 < kTinyMean * kTinyMean};
+                                     std2 > 0.0 && std2 < kTinyStd * kTinyStd, mean2 < kTinyMean * kTinyMean && !sure_nan};
                 atomicAdd(&g_ewk_list[0], 1ull);
                 atomicAdd(&g_ewk_list[5], T);
                 for (int k = 0; k < 4; ++k)

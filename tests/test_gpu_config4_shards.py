@@ -97,14 +97,15 @@ def test_config4_sharded_positives_equal_one_engine(tmp_path):
 
     # every scored event of the 65,536 streams (positives and rejects) against the oracle, and
     # the gathered positives' scores: stream s hears the signal from tick
-    # s on, so events with equal (tick - s, request, length) hold the same samples -- each
-    # distinct segment is scored once by the oracle (tests/oracle_pool.py)
+    # s on (its tick t is signal tick s + t), so events with equal (tick + s, request, length)
+    # hold the same samples -- each distinct segment is scored once by the oracle
+    # (tests/oracle_pool.py)
     from oracle_pool import oracle_scores
     host = sig.cpu().numpy()
     sc_ev = ev[(ev["flags"] & 1) == 0]
     n_req = (sc_ev["tick"].astype(np.int64) * 1600 - sc_ev["ring_start"].astype(np.int64)) % RING
     p0 = sc_ev["tick"].astype(np.int64) * 1600 - n_req                    # offset in the stream
-    key = np.stack([sc_ev["tick"].astype(np.int64) - sc_ev["stream"], n_req, sc_ev["length"].astype(np.int64)], 1)
+    key = np.stack([sc_ev["tick"].astype(np.int64) + sc_ev["stream"], n_req, sc_ev["length"].astype(np.int64)], 1)
     uniq, inv = np.unique(key, axis=0, return_inverse=True)
     inv = inv.reshape(-1)
     first = np.zeros(len(uniq), np.int64)

@@ -172,7 +172,8 @@ def test_config3_streams_full_size_sampled_vs_oracle(env):
     # both paths send the same segments (near the threshold, short, stationary, or with a
     # vanishing MFCC mean vector) to the same fp64 re-score: the ring scores and the batch
     # scores of the same segments agree within the 1e-4 bar
-    small = np.linalg.norm(bm, axis=1) < RESCORE_TINY_MEAN - 0.5   # (a margin for the two paths' float32 means)
+    # (a margin for the two paths' float32 means; a NaN score beyond the float32 error is not listed)
+    small = (np.linalg.norm(bm, axis=1) < RESCORE_TINY_MEAN - 0.5) & np.isfinite(pick["score"])
     assert small.sum() >= 20, int(small.sum())          # the recipe's loud events are covered
     np.testing.assert_array_equal(pick["flags"][small] & 2, 2)
     bad = fin & (d > SCORE_TOL)

@@ -147,7 +147,9 @@ def test_ring_tick_fp64_rescore_in_last_workgroup(template):
         for g, e in zip(mine, ref):
             if e.skipped:
                 continue
-            assert g[7] & 2, (i, g)   # EWK_EV_RESCORED
+            # EWK_EV_RESCORED (a NaN score is listed by the margin only through another criterion,
+            # and a vanishing-mean NaN beyond the float32 error not at all: kNanMarginA)
+            assert g[7] & 2 or np.isnan(g[5]), (i, g)
             cm, cs = mfcc_ref.extract_mfcc(e.audio)
             s = float(mfcc_ref.similarity_from_stats(tm, ts, cm, cs))
             assert score_close(g[5], s, 1e-9), (i, g, s)
