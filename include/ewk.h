@@ -42,7 +42,10 @@ extern "C" {
 
 /* event flags */
 #define EWK_EV_SKIPPED 1      /* segment longer than max_segment_seconds: no level-2 call (wakeword.py:1113-1118) */
-#define EWK_EV_RESCORED 2     /* fp32 score fell inside rescore_margin; decision from the fp64 path */
+#define EWK_EV_RESCORED 2     /* score and decision from the fp64 path: the fp32 score fell inside
+                                 rescore_margin, or the segment is very short (<= 16 frames), nearly
+                                 stationary (|std| < 20) or has a vanishing MFCC mean (|mean| < 32,
+                                 unless its similarity is negative beyond the fp32 error: NaN either way) */
 
 /* ewk_score_segments* flags */
 #define EWK_SCORE_REQUIRE_TEMPLATE 1   /* EWK_ENOTEMPLATE when no template (calculate_similarity) */
