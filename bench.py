@@ -84,6 +84,8 @@ def parse():
     ap.add_argument("--short-len", type=int, default=6400,
                     help="also time the scorer on segments of this length (short_length; 0 = skip)")
     ap.add_argument("--confirm-batch", type=int, default=64, help="config 5: Whisper-tiny batch (0 = skip)")
+    ap.add_argument("--no-pcie", dest="pcie", action="store_false",
+                    help="skip the host-buffer (PCIe-inclusive) pass over the batch")
     ap.add_argument("--no-host-ingest", dest="host_ingest", action="store_false",
                     help="skip the pinned-host ingest legs (streaming_host_ingest)")
     ap.add_argument("--host-streams-f32", type=int, default=131072)
@@ -427,6 +429,30 @@ def fixed_length_bench(torch, dev, ewa, eng, word, n_seg, seed, sh, fixed_len=16
            "matches": int(match.sum().item())}
     del pcm
     return out
+
+
+def pcie_inclusive_bench(torch, eng, pcm, lengths, offsets, frames, reps=3):
+    """The same batch through the host-buffer boundary (ewk_score_segments: the caller's PCM in
+    PINNED host memory, copied to HBM, scored, results copied back, one call per batch): the
+    PCIe-inclusive rate, bounded by the H2D copy of 640 B per frame.  Never the bench `value`."""
+    host = torch.empty(pcm.numel(), dtype=torch.float32, pin_memory=True)
+    host.copy_(pcm)
+    torch.cuda.synchronize()
+    h = host.numpy()
+    off = np.ascontiguousarray(offsets - offsets[0], dtype=np.int64)
+    ln = np.ascontiguousarray(lengths, dtype=np.int32)
+    eng.score_packed(h, off, ln)                # warm-up (device buffers sized)
+    times = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        eng.score_packed(h, off, ln)
+        times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    del host, h
+    return {"boundary": "ewk_score_segments, PCM from pinned host memory, one call per batch (copy in, "
+                        "score, results out; synchronous)", "segments": int(len(ln)), "frames": int(frames),
+            "call_ms_median": t * 1e3, "frames_per_s": frames / t, "h2d_bytes": int(pcm.numel() * 4),
+            "h2d_gbs_effective": pcm.numel() * 4 / t / 1e9}
 
 
 def make_streams(torch, dev, n_streams, seed, word):
@@ -847,6 +873,8 @@ def main():
     # the per-segment fixed cost weighs most
     short = fixed_length_bench(torch, dev, ewa, eng, word, n_seg, args.seed + 1000 * rank, sh,
                                fixed_len=args.short_len) if args.short_len > 0 and world == 1 else None
+    pcie = pcie_inclusive_bench(torch, eng, pcm, lengths, offsets, frames) \
+        if args.pcie and world == 1 else None
     kernel_s = (k_ms / max(1, k_n)) / 1e3
     achieved = frames * BYTES_PER_FRAME / kernel_s / 1e9
     traffic, traffic_src, compute = None, None, None
@@ -913,6 +941,8 @@ def main():
         out["fixed_length"] = fixed
     if short is not None:
         out["short_length"] = short
+    if pcie is not None:
+        out["pcie_inclusive"] = pcie
     if world > 1:   # what the collectives actually ran on (a SCALE run can check RCCL saw N ranks)
         out["distributed"] = {"world_size_seen": dist.get_world_size(), "backend": str(dist.get_backend()),
                               "rccl_version": _rccl_version(torch), "positives_gathered_to_rank0": gathered[0],
