@@ -111,6 +111,15 @@ def test_many_streams_vs_oracle(template):
             n_ev += 1
     if bad:
         from evidence import dump
+        from easywakeword_amd import Engine
+        lin = Engine()
+        lin.set_template(tm, ts)
+        for b in bad:   # the ring's samples now (if not yet overwritten) and the linear scorer's view
+            g = b["mine"]
+            if b["why"] == "score" and L - g[2] * 1600 < 150000:
+                back = eng.read_segment(g[0], g[3], g[1])
+                b["ring_back_linear_score"] = float(lin.score([back], candidate_dtype="float64")[2][0])
+        lin.close()
         path = dump("many_streams", dict(bad=bad, events=got))
         pytest.fail(f"{len(bad)} mismatches (evidence {path}): {bad[:4]}")
     assert n_ev > 20
