@@ -116,7 +116,8 @@ def test_many_streams_vs_oracle(template):
         lin.set_template(tm, ts)
         for b in bad:   # the ring's samples now (if not yet overwritten) and the linear scorer's view
             g = b["mine"]
-            if b["why"] == "score" and L - g[2] * 1600 < 150000:
+            p0 = g[2] * 1600 - (g[2] * 1600 - g[3]) % 160000        # segment start in the stream
+            if b["why"] == "score" and p0 >= L - 150000:                   # not yet overwritten
                 back = eng.read_segment(g[0], g[3], g[1])
                 b["ring_back_linear_score"] = float(lin.score([back], candidate_dtype="float64")[2][0])
         lin.close()
