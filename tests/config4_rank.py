@@ -10,8 +10,11 @@ Rank 0 writes the gathered records [stream, tick, length, score bits] and PCM to
 """
 import os
 import sys
+import time
 
 import numpy as np
+
+t_start = time.time()
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -29,7 +32,10 @@ def main():
 
     out_path, n_total, ticks, seed = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    say = lambda m: print(f"[rank {rank} {time.time() - t_start:.1f} s] {m}", flush=True)
+    say("imports done")
     dist.init_process_group("gloo")
+    say("process group up")
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     word = bench.load_word()
@@ -37,6 +43,7 @@ def main():
     sig = bench.make_shifted_signal(torch, dev, n_total, ticks, seed, word)   # stream s hears it from tick s
     se = ewa.StreamEngine(n)
     se.template_from_pcm(word)
+    say(f"engine with {n} streams")
     cpu = torch.device("cpu")
     col = PositiveCollector(first, cpu, every=10, audio_cap=AUDIO_CAP,
                             audio_fn=lambda e: [a.cpu() for a in se.normalize_events_device(e)])
@@ -55,6 +62,8 @@ def main():
         col.add(se.poll())
         keep(*col.tick(nt))
         t += nt
+        if t % 50 == 0:
+            say(f"tick {t}")
     keep(*col.flush())
     if rank == 0:
         rec = np.concatenate(recs) if recs else np.zeros((0, 4), np.int64)
@@ -64,6 +73,7 @@ def main():
     se.close()
     dist.barrier()
     dist.destroy_process_group()
+    say("done")
 
 
 if __name__ == "__main__":

@@ -30,9 +30,24 @@ def _plain(x):
     return x
 
 
+def _out_dir() -> str:
+    return os.path.join(os.environ.get("GRAFT_REPO_ROOT", ROOT), "gpurun_out")
+
+
+def progress(msg: str) -> None:
+    """Append a timestamped line to gpurun_out/progress.log: a long GPU test's stages (and the
+    heartbeat of tests/conftest.py) stay visible while pytest captures its output."""
+    try:
+        os.makedirs(_out_dir(), exist_ok=True)
+        with open(os.path.join(_out_dir(), "progress.log"), "a") as f:
+            f.write(f"{time.strftime('%H:%M:%S')} {msg}\n")
+    except OSError:
+        pass
+
+
 def dump(name: str, payload: dict) -> str:
     """Write payload to gpurun_out/evidence_<name>_<time>.json; returns the path ('' if unwritable)."""
-    out = os.path.join(os.environ.get("GRAFT_REPO_ROOT", ROOT), "gpurun_out")
+    out = _out_dir()
     try:
         os.makedirs(out, exist_ok=True)
         path = os.path.join(out, f"evidence_{name}_{int(time.time() * 1000)}.json")

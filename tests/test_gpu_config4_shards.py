@@ -62,9 +62,17 @@ def test_config4_sharded_positives_equal_one_engine(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(WORLD),
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "tests", "config4_rank.py"), out, str(N_TOTAL), str(TICKS), str(SEED)]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT,
-                       env=dict(os.environ, OMP_NUM_THREADS="2"))
-    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-3000:])
+    # the ranks' output goes to gpurun_out/ as it is written (stage lines: tests/config4_rank.py)
+    from evidence import _out_dir, progress
+    os.makedirs(_out_dir(), exist_ok=True)
+    log = os.path.join(_out_dir(), "config4_ranks.log")
+    with open(log, "w") as f:
+        r = subprocess.run(cmd, stdout=f, stderr=subprocess.STDOUT, text=True, timeout=600, cwd=ROOT,
+                           env=dict(os.environ, OMP_NUM_THREADS="2"))
+    with open(log) as f:
+        tail = f.read()[-3000:]
+    assert r.returncode == 0, tail
+    progress("config4: ranks done, single engine")
     got = np.load(out)
     assert int(got["world"]) == WORLD
     rec = got["rec"]
@@ -101,6 +109,7 @@ def test_config4_sharded_positives_equal_one_engine(tmp_path):
     # hold the same samples -- each distinct segment is scored once by the oracle
     # (tests/oracle_pool.py)
     from oracle_pool import oracle_scores
+    progress(f"config4: {len(pos)} positives, oracle over the events")
     host = sig.cpu().numpy()
     sc_ev = ev[(ev["flags"] & 1) == 0]
     n_req = (sc_ev["tick"].astype(np.int64) * 1600 - sc_ev["ring_start"].astype(np.int64)) % RING
