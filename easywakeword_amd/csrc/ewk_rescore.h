@@ -24,7 +24,7 @@
 //   c_k = A_k + theta B_k,  A_k = sum_{x >= theta} D_km x_m,  B_k = sum_{x < theta} D_km,
 // exact for the true theta as long as no value lies within kRsWindow of theta_s (then the
 // classification x >= theta_s equals x >= theta); a chunk holding such a value is recomputed
-// with the exact theta by the wave that finishes the slot (rare: ~0.1 value per segment).
+// with the exact theta by the wave that finishes the slot (rare: ~1 chunk in 1,000-5,000).
 // The chunk's sums (shifted by its first frame: identical frames give an exact 0 std) go to
 // a part record; the finishing wave merges the parts in chunk order as polynomials in theta,
 // so the result does not depend on which waves ran which chunks (MODE 0, 1, 2 and the
@@ -37,6 +37,7 @@
 #ifdef EWK_RS_TIMING
 __device__ unsigned long long g_rs_dbg[16];
 #define EWK_RS_ADD(k, v) (void)atomicAdd(&g_rs_dbg[k], (unsigned long long)(v))
+#define EWK_RS_MAX(k, v) (void)atomicMax(&g_rs_dbg[k], (unsigned long long)(v))
 // chunk sub-phases (s_memtime cycles summed over chunks): 0 samples + window, 1 FFT stages,
 // 2 untangle + power, 3 mel + log10, 4 DCT, 5 sums + flags, 6 chunks, 7 frame groups
 // (summed in registers, flushed once per chunk: an atomic inside the frame loop would put a
@@ -48,13 +49,21 @@ __device__ unsigned long long g_rs_ph[8];
 #define EWK_RS_ARG , rph
 #else
 #define EWK_RS_ADD(k, v) ((void)0)
+#define EWK_RS_MAX(k, v) ((void)0)
 #define EWK_RS_TS(v)
 #define EWK_RS_PH(k, a, b) ((void)0)
 #define EWK_RS_PARAM
 #define EWK_RS_ARG
 #endif
 
-constexpr double kRsWindow = 1e-3;   // dB; the float32 max is within ~1e-5 dB of the fp64 one
+// dB.  Measured (scripts/rs_window_probe.py, every segment of the bench batch at three lengths and
+// of four other recipes listed: ~210,000 segments): |theta - theta_s| <= 1.98e-5 dB, so 2e-4 keeps a
+// 10x margin; a wider window only recomputes more chunks (1e-3: 61 of 16,358 bench chunks,
+// 516 of 16,376 stationary ones), a slot beyond it redoes every chunk (correct, slower).
+#ifndef EWK_RS_WINDOW
+#define EWK_RS_WINDOW 2e-4
+#endif
+constexpr double kRsWindow = EWK_RS_WINDOW;
 constexpr double kRsTopDb = 80.0;
 
 // What the drain needs of ScoreArgs, copied in score_tail: the drain is a real call (its
@@ -639,6 +648,7 @@ __device__ void rs_finish(const RsArgs& a, RsSlot* sp, int seg, int T, float the
     const bool nan_in = (fl & 2) != 0;
     const bool redo_all = !(fabs(theta - theta_s) <= kRsWindow);
     if (lane == 0 && parts) { EWK_RS_ADD(6, redo_all); EWK_RS_ADD(7, nch); }
+    if (lane == 0 && !nan_in && theta == theta) EWK_RS_MAX(14, fmin(fabs(theta - theta_s), 1e9) * 1e9);   // (1e-9 dB units)
     if (!nan_in && (parts || redo_all || (fl & 1))) {
         if (!parts) acc = RsAcc();
         // the part records are read one chunk ahead of their merge (uncached memory: a round

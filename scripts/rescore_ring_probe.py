@@ -34,6 +34,7 @@ if dbg:
     if hasattr(dlib, "ewk_debug_rs_ph"):
         dlib.ewk_debug_rs_ph((ctypes.c_ulonglong * 8)())
 rows = []
+dmax = [0]
 for i in range(ticks):
     k = t % period
     se.profile(True)
@@ -52,7 +53,8 @@ for i in range(ticks):
             print(f"  tick {i}: drain waves {d[0]} wgs {d[9]} chunks {d[1]} ({d[2] / max(1, d[1]):,.0f} cyc each) "
                   f"finishes {d[3]} ({d[4] / max(1, d[3]):,.0f} cyc each) serial {d[5]} redo_all {d[6]} "
                   f"chunks-in-finished {d[7]} recomputed {d[8]}; drain per wave max {d[10] / 100:.0f} us mean {d[11] / 100 / max(1, d[0]):.0f} us; "
-                  f"claim scans {d[12]}; last-WG tail {d[13] / 100:.1f} us")
+                  f"claim scans {d[12]}; last-WG tail {d[13] / 100:.1f} us; max |theta - theta_s| {d[14] * 1e-9:.2e} dB")
+            dmax[0] = max(dmax[0], d[14])
     T = 1 + rs["length"].astype(np.int64) // 160
     rows.append((len(real), len(rs), int(T.sum()), int(((T + 7) // 8).sum()), int(T.max()) if len(T) else 0, sc_ms * 1e3, r_ms * 1e3))
     t += 1
@@ -76,3 +78,5 @@ if sel.any():
 if (~sel).any():
     print("ticks with listed events: %d, rescore %.1f us, per chunk %.2f us, per max-T frame %.2f us" % (
         (~sel).sum(), a[~sel, 6].mean(), (a[~sel, 6] / a[~sel, 3]).mean(), (a[~sel, 6] / np.maximum(a[~sel, 4], 1)).mean()))
+if dbg:
+    print(f"max |theta - theta_s| over the listed segments: {dmax[0] * 1e-9:.3e} dB (window {os.environ.get('EWK_RS_WINDOW_NOTE', '')})")
