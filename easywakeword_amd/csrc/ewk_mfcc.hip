@@ -85,6 +85,21 @@ __device__ unsigned long long g_ewk_dbg[kDbgN];
 #ifdef EWK_LIST_STATS
 __device__ unsigned long long g_ewk_list[10];
 #endif
+#ifdef EWK_COOP_DEBUG
+// what each wave of the cooperative ring scorer saw, keyed by (stream & 31) * 256 + (tick & 255)
+// (scripts/diag_coop.py): the event, its max/min/theta, its shifted sums, the combined stats
+constexpr int kCoopKeys = 32 * 256;
+__device__ int4 g_coop_ev[kCoopKeys][WAVES];      // stream, ring_start, length, tick
+__device__ float4 g_coop_th[kCoopKeys][WAVES];    // wave vmax, wave vmin, theta, nloc
+__device__ double g_coop_pd[kCoopKeys][WAVES][60];
+__device__ float g_coop_ms[kCoopKeys][40];
+__device__ uint4 g_coop_tile[4 * 256][WAVES][512];   // streams 0-3: each wave's last tile before the clamp
+#define EWK_COOP_KEY_PARAM , int dkey
+#define EWK_COOP_KEY_ARG(k) , (k)
+#else
+#define EWK_COOP_KEY_PARAM
+#define EWK_COOP_KEY_ARG(k)
+#endif
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
@@ -1313,7 +1328,7 @@ __device__ void segment_stats(const SegSrc<RING>& v, const unsigned char* smem, 
 template <int RING>
 __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, float* scr, float* tile,
                                    float* spec, int wave, int lane, const int (&lo)[8], float* misc0,
-                                   float& theta_out) {
+                                   float& theta_out EWK_COOP_KEY_PARAM) {
     const float* s_dct = reinterpret_cast<const float*>(smem + L_DCT);
     float* wg_mm = reinterpret_cast<float*>(smem + L_WG + 16);   // [WAVES][2] max, min
     const int T = 1 + v.len / HOP;
@@ -1338,6 +1353,13 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
         tile_passes(v, tile_i, T, smem, scr, tile, lane, lo, vmax, tmin, nanp, run);
         const float tmw = wave_min(tmin);
         vmin = fminf(vmin, tmw);
+#ifdef EWK_COOP_DEBUG
+        if (last && dkey < 4 * 256) {
+            lds_order();
+#pragma unroll
+            for (int u = 0; u < 8; ++u) g_coop_tile[dkey][wave][64 * u + lane] = reinterpret_cast<const uint4*>(tile)[64 * u + lane];
+        }
+#endif
         if (last) { last_min = tmw; break; }
         const float run2 = rec ? wave_max(vmax) - kTopDbUnits : -INFINITY;
         if (run2 > run && tmw < run2) {   // self-clamp (segment_stats)
@@ -1367,6 +1389,9 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
     for (int w = 0; w < WAVES; ++w) { vmax = fmaxf(vmax, wg_mm[2 * w]); vmin = fminf(vmin, wg_mm[2 * w + 1]); }
     const float theta = vmax - kTopDbUnits;
     theta_out = theta;
+#ifdef EWK_COOP_DEBUG
+    if (lane == 0) g_coop_th[dkey][wave] = make_float4(wg_mm[2 * wave], wg_mm[2 * wave + 1], theta, (float)nloc);
+#endif
     if (nloc > 0) {
         const int tile_l = wave + WAVES * (nloc - 1);
         if (last_min < theta) {   // the last tile, still in LDS: clamp at the final threshold
@@ -1413,6 +1438,9 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
         }
     }
     __syncthreads();
+#ifdef EWK_COOP_DEBUG
+    if (lane < 60) g_coop_pd[dkey][wave][lane] = pd[lane];
+#endif
     if (wave == 0) {
         double mean = 0.0, sd = 0.0;
         if (lane < NMFCC) {
@@ -1435,6 +1463,9 @@ __device__ void segment_stats_coop(const SegSrc<RING>& v, unsigned char* smem, f
         }
         lds_order();
         if (lane < NMFCC) { misc0[lane] = (float)mean; misc0[20 + lane] = (float)sd; }
+#ifdef EWK_COOP_DEBUG
+        if (lane < NMFCC) { g_coop_ms[dkey][lane] = (float)mean; g_coop_ms[dkey][20 + lane] = (float)sd; }
+#endif
         lds_order();
     }
 }
@@ -1721,7 +1752,11 @@ __global__ __launch_bounds__(64 * WAVES, 1) void k_score_f32(const Tables* __res
                     static_cast<const unsigned char*>(ring_base) + (int64_t)ev.stream * a.ring_len * sample_bytes(RING),
                     ev.ring_start, a.ring_len, ev.length);
                 float theta_s;
-                segment_stats_coop(v, smem, scr, tile, spec, wave, lane, lo, misc0, theta_s);
+#ifdef EWK_COOP_DEBUG
+                const int dkey = (ev.stream & 31) * 256 + (int)(ev.tick & 255);
+                if (lane == 0) g_coop_ev[dkey][wave] = make_int4(ev.stream, (int)ev.ring_start, ev.length, (int)ev.tick);
+#endif
+                segment_stats_coop(v, smem, scr, tile, spec, wave, lane, lo, misc0, theta_s EWK_COOP_KEY_ARG(dkey));
                 if (wave == 0 && (a.has_template || a.list_all))
                     score_epilogue<RING>(a, act ? misc0[lane] : 0.0f, act ? misc0[20 + lane] : 0.0f, tmf, tsf, lane,
                                          seg, v.len, theta_s);
@@ -1803,6 +1838,24 @@ extern "C" int ewk_debug_rs_ph(unsigned long long* out) {   // chunk sub-phase c
     unsigned long long z[8] = {};
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ewk::g_rs_ph), sizeof(z)) != hipSuccess) return -3;
     if (hipMemcpyToSymbol(HIP_SYMBOL(ewk::g_rs_ph), z, sizeof(z)) != hipSuccess) return -3;
+    return 0;
+}
+namespace ewk {
+#endif
+
+#ifdef EWK_COOP_DEBUG
+}  // namespace ewk
+extern "C" int ewk_debug_coop(void* ev, void* th, void* pd, void* ms) {   // debug builds only
+    if (hipMemcpyFromSymbol(ev, HIP_SYMBOL(ewk::g_coop_ev), sizeof(ewk::g_coop_ev)) != hipSuccess) return -3;
+    if (hipMemcpyFromSymbol(th, HIP_SYMBOL(ewk::g_coop_th), sizeof(ewk::g_coop_th)) != hipSuccess) return -3;
+    if (hipMemcpyFromSymbol(pd, HIP_SYMBOL(ewk::g_coop_pd), sizeof(ewk::g_coop_pd)) != hipSuccess) return -3;
+    if (hipMemcpyFromSymbol(ms, HIP_SYMBOL(ewk::g_coop_ms), sizeof(ewk::g_coop_ms)) != hipSuccess) return -3;
+    return 0;
+}
+extern "C" int ewk_debug_coop_tile(int key, void* out) {   // one key's [WAVES][512] uint4 (debug builds only)
+    if (key < 0 || key >= 4 * 256) return -1;
+    const size_t one = sizeof(ewk::g_coop_tile[0]);
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ewk::g_coop_tile), one, (size_t)key * one) != hipSuccess) return -3;
     return 0;
 }
 namespace ewk {

@@ -109,6 +109,18 @@ def test_many_streams_vs_oracle(template):
             if not score_close(g[5], s, 1e-4) or bool(g[6]) != (s >= 75.0):
                 bad.append(dict(stream=i, why="score", mine=g, oracle=s))
             n_ev += 1
+            # the ring still holding this segment (the last 10 s): its samples, bit for bit
+            p0 = g[2] * 1600 - (g[2] * 1600 - g[3]) % 160000        # segment start in the stream
+            if p0 >= L - 160000:
+                back = eng.read_segment(i, g[3], g[1])
+                want = np.asarray(e.audio, np.float32)
+                diff = np.nonzero(back != want)[0]
+                if len(diff):
+                    j = p0 + diff[:64]
+                    bad.append(dict(stream=i, why="ring", mine=g, n_diff=int(len(diff)), first=int(diff[0]),
+                                    last=int(diff[-1]), idx=diff[:64], got=back[diff[:64]], want=want[diff[:64]],
+                                    stale=data[i][np.maximum(j - 160000, 0)], tick_before=data[i][np.maximum(j - 1600, 0)],
+                                    other_streams=[int(k) for k in np.nonzero((data[:, j[0]] == back[diff[0]]))[0]]))
     if bad:
         from evidence import dump
         from easywakeword_amd import Engine
@@ -121,6 +133,24 @@ def test_many_streams_vs_oracle(template):
                 back = eng.read_segment(g[0], g[3], g[1])
                 b["ring_back_linear_score"] = float(lin.score([back], candidate_dtype="float64")[2][0])
         lin.close()
+        from easywakeword_amd import _lib
+        lib = _lib.load()
+        if hasattr(lib, "ewk_debug_coop"):   # -DEWK_COOP_DEBUG builds: what each wave of the scorer saw
+            ev = np.zeros((8192, 8, 4), np.int32)
+            th = np.zeros((8192, 8, 4), np.float32)
+            pd = np.zeros((8192, 8, 60), np.float64)
+            ms = np.zeros((8192, 40), np.float32)
+            import ctypes
+            vp = lambda a: ctypes.c_void_p(a.ctypes.data)   # (a bare int would pass as a 32-bit C int)
+            if lib.ewk_debug_coop(vp(ev), vp(th), vp(pd), vp(ms)) == 0:
+                for b in bad:
+                    g = b["mine"]
+                    key = (g[0] & 31) * 256 + (g[2] & 255)
+                    b["coop"] = dict(ev=ev[key], th=th[key], pd=pd[key], ms=ms[key])
+                    if key < 1024 and hasattr(lib, "ewk_debug_coop_tile"):
+                        tl = np.zeros((8, 512, 4), np.uint32)
+                        if lib.ewk_debug_coop_tile(ctypes.c_int(key), vp(tl)) == 0:
+                            b["coop"]["tile"] = tl
         path = dump("many_streams", dict(bad=bad, events=got))
         pytest.fail(f"{len(bad)} mismatches (evidence {path}): {bad[:4]}")
     assert n_ev > 20
