@@ -740,7 +740,11 @@ int ewk_reset_streams(ewk_engine* e) {
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = e->stream;
     HIP_TRY(join_scoring(e, s));
+#ifndef EWK_RING_MEMSET
+    HIP_TRY(launch_ring_zero(e->d_ring, (size_t)e->n_streams * e->sring_len * e->ring_es, s));
+#else   // (the round-6 fill, kept for the A/B of scripts/gpu_miss_prefix.sh)
     HIP_TRY(hipMemsetAsync(e->d_ring, 0, (size_t)e->n_streams * e->sring_len * e->ring_es, s));
+#endif
     HIP_TRY(hipMemsetAsync(e->d_brms, 0, (size_t)e->n_streams * std::max(1, e->n_blocks) * sizeof(double), s));
     std::vector<GateStream> st(e->n_streams);
     for (auto& x : st) {

@@ -92,6 +92,9 @@ struct GateArgs {
 
 hipError_t launch_gate(const GateArgs& g, hipStream_t s);
 hipError_t launch_reenter(GateStream* st, int32_t first, int32_t n, double tick_seconds, hipStream_t s);
+// Zero a ring with agent-scope (sc1) stores: the lines go to memory and are dropped from the
+// writing XCD's L2, so no cached copy of the initial zeros outlives the gate's first writes.
+hipError_t launch_ring_zero(void* p, size_t bytes, hipStream_t s);
 // register-resident block RMS arrays up to 64 * kGateRegMax blocks (10 s ring: block >= 313 samples)
 constexpr int kGateRegMax = 8;
 int gate_val_len(const PwTree* trees_host, int n_blocks);

@@ -929,6 +929,24 @@ __global__ void k_reenter(GateStream* st, int32_t first, int32_t n, double tick_
     st[i] = s;
 }
 
+// Ring initialisation (ewk_reset_streams).  Round 6's recording build caught the ring scorer
+// reading four 128-B lines of ZEROS -- the ring's initial fill -- where the gate had written
+// samples twice since ("The ring-path miss recurred"); the fill used
+// hipMemsetAsync.  Here every line is written by an agent-scope store (global_store sc1:
+// performed at memory, not kept in the XCD's L2), 8 B per lane.
+__global__ void k_ring_zero(uint64_t* p, size_t n8) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x)
+        __hip_atomic_store(p + i, (uint64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+hipError_t launch_ring_zero(void* p, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    if (bytes % 8 || ((uintptr_t)p & 7)) return hipErrorInvalidValue;
+    const size_t n8 = bytes / 8;
+    const unsigned grid = (unsigned)std::min<size_t>(4096, (n8 + 255) / 256);
+    hipLaunchKernelGGL(k_ring_zero, dim3(grid), dim3(256), 0, s, static_cast<uint64_t*>(p), n8);
+    return hipGetLastError();
+}
+
 hipError_t launch_reenter(GateStream* st, int32_t first, int32_t n, double tick_seconds, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_reenter, dim3((n + 255) / 256), dim3(256), 0, s, st, first, n, tick_seconds);

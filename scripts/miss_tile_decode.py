@@ -18,6 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "tests"))
 sys.path.insert(0, os.path.join(HERE, ".."))
 sys.path.insert(0, HERE)
+EVIDENCE = sys.argv.pop(1) if len(sys.argv) > 1 else ""   # (miss_r05 reads sys.argv at import)
 
 import miss_r05  # noqa: E402
 import miss_r06  # noqa: E402
@@ -38,7 +39,7 @@ def decode(tile_u32):
 
 
 def main():
-    d = json.load(open(sys.argv[1]))
+    d = json.load(open(EVIDENCE))
     data = miss_r05.scenario()
     cfg = GateConfig(pre_speech_silence=0.8, speech_duration_min=0.3, speech_duration_max=2.0, post_speech_silence=0.4)
     for b in d["bad"]:
